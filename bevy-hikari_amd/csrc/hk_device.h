@@ -1,0 +1,892 @@
+// hk_device.h — device-side building blocks of the gfx950 integrator.
+//
+// Semantics follow src/shaders/light.wgsl / denoise.wgsl exactly (same operation order,
+// same IEEE single rounding, transcendentals from include/hk_math.h, compiled with
+// -ffp-contract=off) so that results are bit-identical to the CPU oracle.  The memory
+// layout is MI355X-first instead of the reference's:
+//   * reservoirs are stored as 4 SoA planes of 16-byte chunks (plane k = bytes 16k..16k+15
+//     of every PackedReservoir), so a wave reads/writes 4 x 1 KiB fully coalesced;
+//   * G-buffer / render targets are row-major planes (one per texture);
+//   * scene records keep the std430 boundary layout (they are L2/MALL resident) and are
+//     fetched with 16-byte vector loads.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hk_math.h"
+#include "../../include/hk_types.h"
+#include "../../include/hikari_amd.h"
+
+namespace hk {
+
+// ------------------------------------------------------------------ vectors
+struct f2 {
+    float x, y;
+};
+struct f3 {
+    float x, y, z;
+};
+struct f4 {
+    float x, y, z, w;
+};
+#define HKD __device__ __forceinline__
+HKD f2 mk2(float x, float y) { return f2{x, y}; }
+HKD f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+HKD f4 mk4(float x, float y, float z, float w) { return f4{x, y, z, w}; }
+HKD f3 xyz(f4 a) { return mk3(a.x, a.y, a.z); }
+HKD f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+HKD f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+HKD f3 operator*(f3 a, f3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+HKD f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+HKD f3 operator/(f3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
+HKD float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+HKD float dot(f2 a, f2 b) { return a.x * b.x + a.y * b.y; }
+HKD f3 cross(f3 a, f3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+HKD float length(f3 a) { return sqrtf(dot(a, a)); }
+HKD f3 normalize(f3 a) { return a * (1.0f / sqrtf(dot(a, a))); }
+HKD f3 vmin(f3 a, f3 b) { return mk3(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
+HKD f3 vmax(f3 a, f3 b) { return mk3(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
+HKD f3 mix(f3 a, f3 b, float t)
+{
+    float it = 1.0f - t;
+    return mk3(a.x * it + b.x * t, a.y * it + b.y * t, a.z * it + b.z * t);
+}
+HKD f3 inv(f3 d) { return mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+HKD float sum4(f4 a) { return ((a.x + a.y) + a.z) + a.w; }
+HKD float lum(f3 c) { return hk_luminance(c.x, c.y, c.z); }
+HKD f3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+
+HKD uint32_t f2u32(float x)
+{
+    if (!(x > 0.0f)) return 0u;
+    if (x >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)x;
+}
+HKD int32_t f2i32(float x)
+{
+    if (x != x) return 0;
+    if (x >= 2147483648.0f) return 0x7FFFFFFF;
+    if (x <= -2147483648.0f) return (int32_t)0x80000000u;
+    return (int32_t)x;
+}
+HKD uint32_t umod(uint32_t a, uint32_t b) { return b ? a % b : 0u; }
+
+HKD f4 mat4_mul(const float* m, f4 v)
+{
+    f4 r;
+    r.x = ((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * v.w;
+    r.y = ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * v.w;
+    r.z = ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * v.w;
+    r.w = ((m[3] * v.x + m[7] * v.y) + m[11] * v.z) + m[15] * v.w;
+    return r;
+}
+
+// ------------------------------------------------------------------ constants (light.wgsl:226-256)
+constexpr float RAY_BIAS = 0.02f;
+constexpr float DISTANCE_MAX = 65535.0f;
+constexpr float MAX_VARIANCE = 10.0f;
+constexpr uint32_t DONT_EXCLUDE = 0xFFFFFFFFu;
+constexpr uint32_t DONT_SAMPLE_EMISSIVE = 0x80000000u;
+
+// ------------------------------------------------------------------ kernel parameter blocks
+struct Scene {
+    const hk_vertex* vertices;
+    const hk_primitive* primitives;
+    const hk_node* asset_nodes;
+    const hk_alias_entry* alias_table;
+    const hk_instance* instances;
+    const hk_node* instance_nodes;
+    const hk_material* materials;
+    const hk_node* emissive_nodes;
+    const hk_emissive* emissives;
+    uint32_t n_instances, n_instance_nodes, n_materials, n_emissive_nodes;
+};
+
+// Frame-uniform + view + lights constants (view.rs:105-123, mesh_view_bindings.wgsl).
+struct Frame {
+    uint32_t number;
+    uint32_t direct_validate_interval, emissive_validate_interval;
+    uint32_t max_temporal_reuse_count, max_spatial_reuse_count;
+    uint32_t indirect_bounces, temporal_reuse;
+    float max_reservoir_lifetime, max_indirect_luminance, upscale_ratio;
+    float cos_solar_angle;  // cos(frame.solar_angle), computed once per frame with hk_cos
+    float clear_color[4];
+    float view_world_position[3];
+    float view_proj_z[3];   // view_proj[0].z, [1].z, [2].z (orthographic view vector)
+    int orthographic;       // view.projection[3].w == 1.0
+    float directional_color[3];
+    float direction_to_light[3];
+    float ambient_color[3];
+    // sizes: S = deferred (physical), s = integrator; band = rows [row0, row0+rows) of the
+    // global frame held in the local buffers (whole frame: 0, H)
+    uint32_t S[2], s[2];
+    int32_t S_row0, S_rows;  // deferred-plane band
+    int32_t s_row0, s_rows;  // integrator-plane band
+};
+
+// Row-major planes of the deferred (G-buffer) textures, band-local.
+struct GBuffer {
+    float4* position;
+    uint32_t* normal;
+    float2* depth_gradient;
+    float2* instance_material;
+    float4* velocity_uv;
+};
+
+// SoA reservoir buffer: 4 planes of N 16-byte chunks.
+struct ResBuf {
+    uint4* base;
+    uint32_t n;  // records per plane
+};
+
+struct Counters {
+    unsigned long long* top;
+    unsigned long long* emitter;
+    unsigned long long* primary;
+};
+
+// ------------------------------------------------------------------ texel access
+HKD void store_rgba16f(uint2* tex, int32_t idx, f4 c)
+{
+    uint32_t a = hk_f32_to_f16(c.x) | (hk_f32_to_f16(c.y) << 16);
+    uint32_t b = hk_f32_to_f16(c.z) | (hk_f32_to_f16(c.w) << 16);
+    tex[idx] = make_uint2(a, b);
+}
+HKD f4 load_rgba16f(const uint2* tex, int32_t idx)
+{
+    uint2 v = tex[idx];
+    return mk4(hk_unpack_lo16float(v.x), hk_unpack_hi16float(v.x), hk_unpack_lo16float(v.y), hk_unpack_hi16float(v.y));
+}
+
+// Deferred-texture addressing: frame-OOB -> 0 (textureLoad robustness); in-frame rows outside
+// the band are clamped into it (those values only feed discarded halo pixels).
+HKD bool in_frame(int32_t x, int32_t y, const uint32_t* size)
+{
+    return x >= 0 && y >= 0 && (uint32_t)x < size[0] && (uint32_t)y < size[1];
+}
+HKD int32_t band_index(int32_t x, int32_t y, uint32_t width, int32_t row0, int32_t rows)
+{
+    int32_t ly = y - row0;
+    ly = ly < 0 ? 0 : (ly >= rows ? rows - 1 : ly);
+    return x + (int32_t)width * ly;
+}
+HKD f4 load_position(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
+{
+    if (!in_frame(x, y, F.S)) return mk4(0, 0, 0, 0);
+    float4 p = G.position[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    return mk4(p.x, p.y, p.z, p.w);
+}
+HKD float load_depth(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
+{
+    if (!in_frame(x, y, F.S)) return 0.0f;
+    return G.position[band_index(x, y, F.S[0], F.S_row0, F.S_rows)].w;
+}
+HKD f3 load_normal(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
+{
+    if (!in_frame(x, y, F.S)) return mk3(0, 0, 0);
+    uint32_t n = G.normal[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    return mk3(hk_unpack_snorm8(n, 0), hk_unpack_snorm8(n, 1), hk_unpack_snorm8(n, 2));
+}
+HKD f2 load_instance_material(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
+{
+    if (!in_frame(x, y, F.S)) return mk2(0, 0);
+    float2 v = G.instance_material[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    return mk2(v.x, v.y);
+}
+HKD f4 load_velocity_uv(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
+{
+    if (!in_frame(x, y, F.S)) return mk4(0, 0, 0, 0);
+    float4 v = G.velocity_uv[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    return mk4(v.x, v.y, v.z, v.w);
+}
+HKD f2 load_depth_gradient(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
+{
+    if (!in_frame(x, y, F.S)) return mk2(0, 0);
+    float2 v = G.depth_gradient[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    return mk2(v.x, v.y);
+}
+// integrator-plane (s) index of an in-frame pixel
+HKD int32_t s_index(const Frame& F, int32_t x, int32_t y) { return band_index(x, y, F.s[0], F.s_row0, F.s_rows); }
+
+HKD f2 coords_to_uv(int32_t x, int32_t y, const uint32_t* size)
+{
+    return mk2(((float)x + 0.5f) / (float)size[0], ((float)y + 0.5f) / (float)size[1]);
+}
+// light.wgsl:1007-1017 (jitter 0.25) / denoise.wgsl:37-41 (jitter 0.5)
+HKD f2 jittered_uv(const Frame& F, f2 uv, float amount)
+{
+    float tx = 1.0f / (float)F.S[0], ty = 1.0f / (float)F.S[1];
+    float ratio = F.upscale_ratio - 1.0f;
+    float j = (F.number & 1u) == 0u ? -amount : amount;
+    return mk2(uv.x + (j * tx) * ratio, uv.y + (j * ty) * ratio);
+}
+HKD void jittered_coords(const Frame& F, f2 uv, int32_t& x, int32_t& y)
+{
+    f2 d = jittered_uv(F, uv, 0.25f);
+    x = f2i32(d.x * (float)F.S[0]);
+    y = f2i32(d.y * (float)F.S[1]);
+}
+HKD void nearest_texel(f2 uv, const uint32_t* size, int32_t& x, int32_t& y)
+{
+    int32_t ix = f2i32(floorf(uv.x * (float)size[0]));
+    int32_t iy = f2i32(floorf(uv.y * (float)size[1]));
+    x = ix < 0 ? 0 : (ix > (int32_t)size[0] - 1 ? (int32_t)size[0] - 1 : ix);
+    y = iy < 0 ? 0 : (iy > (int32_t)size[1] - 1 ? (int32_t)size[1] - 1 : iy);
+}
+
+// ------------------------------------------------------------------ reservoirs (light.wgsl:45-223)
+struct Sample {
+    f4 radiance;
+    f4 random;
+    f4 visible_position;
+    f3 visible_normal;
+    uint32_t visible_instance;
+    f4 sample_position;
+    f3 sample_normal;
+};
+struct Reservoir {
+    Sample s;
+    float count, lifetime, w, w_sum, w2_sum;
+};
+HKD Sample zero_sample()
+{
+    Sample s;
+    s.radiance = s.random = s.visible_position = s.sample_position = mk4(0, 0, 0, 0);
+    s.visible_normal = s.sample_normal = mk3(0, 0, 0);
+    s.visible_instance = 0u;
+    return s;
+}
+HKD Reservoir zero_reservoir()
+{
+    Reservoir r;
+    r.s = zero_sample();
+    r.count = r.lifetime = r.w = r.w_sum = r.w2_sum = 0.0f;
+    return r;
+}
+
+HKD Reservoir unpack_reservoir(uint4 c0, uint4 c1, uint4 c2, uint4 c3)
+{
+    Reservoir r;
+    r.count = hk_unpack_lo16float(c3.z);
+    r.w = hk_unpack_hi16float(c3.z);
+    r.w_sum = hk_unpack_lo16float(c3.w);
+    r.w2_sum = hk_unpack_hi16float(c3.w);
+    r.s.radiance = mk4(hk_unpack_lo16float(c0.x), hk_unpack_hi16float(c0.x), hk_unpack_lo16float(c0.y),
+                       hk_unpack_hi16float(c0.y));
+    r.s.random = mk4(hk_unpack_unorm16(c0.z), hk_unpack_unorm16(c0.z >> 16), hk_unpack_unorm16(c0.w),
+                     hk_unpack_unorm16(c0.w >> 16));
+    r.s.visible_position = mk4(__uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z), __uint_as_float(c1.w));
+    uint32_t vn = c3.x;
+    r.s.visible_normal = normalize(mk3(hk_unpack_snorm8(vn, 0), hk_unpack_snorm8(vn, 1), hk_unpack_snorm8(vn, 2)));
+    r.lifetime = 127.0f * (1.0f + hk_unpack_snorm8(vn, 3));
+    uint32_t sn = c3.y;
+    r.s.sample_position = mk4(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z), hk_unpack_snorm8(sn, 3));
+    r.s.sample_normal = normalize(mk3(hk_unpack_snorm8(sn, 0), hk_unpack_snorm8(sn, 1), hk_unpack_snorm8(sn, 2)));
+    r.s.visible_instance = f2u32(__uint_as_float(c2.w));
+    return r;
+}
+HKD Reservoir load_res(const ResBuf& b, int32_t i)
+{
+    const uint4* p = b.base;
+    return unpack_reservoir(p[i], p[b.n + i], p[2 * b.n + i], p[3 * b.n + i]);
+}
+HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
+{
+    uint4 c0, c1, c2, c3;
+    c3.z = hk_pack2x16float(r.count, r.w);
+    c3.w = hk_pack2x16float(r.w_sum, r.w2_sum);
+    c0.x = hk_pack2x16float(r.s.radiance.x, r.s.radiance.y);
+    c0.y = hk_pack2x16float(r.s.radiance.z, r.s.radiance.w);
+    c0.z = hk_pack2x16unorm(r.s.random.x, r.s.random.y);
+    c0.w = hk_pack2x16unorm(r.s.random.z, r.s.random.w);
+    c1 = make_uint4(__float_as_uint(r.s.visible_position.x), __float_as_uint(r.s.visible_position.y),
+                    __float_as_uint(r.s.visible_position.z), __float_as_uint(r.s.visible_position.w));
+    c2 = make_uint4(__float_as_uint(r.s.sample_position.x), __float_as_uint(r.s.sample_position.y),
+                    __float_as_uint(r.s.sample_position.z), __float_as_uint((float)r.s.visible_instance));
+    c3.x = hk_pack4x8snorm(r.s.visible_normal.x, r.s.visible_normal.y, r.s.visible_normal.z, r.lifetime / 127.0f - 1.0f);
+    c3.y = hk_pack4x8snorm(r.s.sample_normal.x, r.s.sample_normal.y, r.s.sample_normal.z, r.s.sample_position.w);
+    uint4* p = b.base;
+    p[i] = c0;
+    p[b.n + i] = c1;
+    p[2 * b.n + i] = c2;
+    p[3 * b.n + i] = c3;
+}
+
+HKD void set_reservoir(Reservoir& r, const Sample& s, float w_new)
+{
+    r.count = 1.0f;
+    r.lifetime = 0.0f;
+    r.w_sum = w_new;
+    r.w2_sum = w_new * w_new;
+    r.s = s;
+}
+HKD void update_reservoir(Reservoir& r, const Sample& s, float w_new)
+{
+    r.w_sum += w_new;
+    r.w2_sum += w_new * w_new;
+    r.count = r.count + 1.0f;
+    float rand = hk_fract(sum4(s.random));
+    if (rand < w_new / r.w_sum) r.s = s;
+}
+HKD void merge_reservoir(Reservoir& r, const Reservoir& other, float p)
+{
+    float count = r.count;
+    update_reservoir(r, other.s, (p * other.w) * other.count);
+    r.count = count + other.count;
+}
+HKD bool uv_inside_open(f2 uv) { return fabsf(uv.x - 0.5f) < 0.5f && fabsf(uv.y - 0.5f) < 0.5f; }
+HKD bool uv_inside_closed(f2 uv) { return fabsf(uv.x - 0.5f) <= 0.5f && fabsf(uv.y - 0.5f) <= 0.5f; }
+
+HKD Reservoir load_previous(const Frame& F, const ResBuf& b, f2 uv)
+{
+    if (uv_inside_open(uv)) {
+        int32_t x = f2i32(uv.x * (float)F.s[0]);
+        int32_t y = f2i32(uv.y * (float)F.s[1]);
+        return load_res(b, s_index(F, x, y));
+    }
+    return zero_reservoir();
+}
+
+HKD bool check_previous_reservoir(Reservoir& r, const Sample& s)
+{
+    float depth_ratio = r.s.visible_position.w / s.visible_position.w;
+    depth_ratio = depth_ratio < 1.0f ? 1.0f / depth_ratio : depth_ratio;
+    bool depth_miss = depth_ratio > 1.05f * (1.0f + 0.5f * s.random.x);
+    bool instance_miss = r.s.visible_instance != s.visible_instance;
+    bool normal_miss = dot(s.visible_normal, r.s.visible_normal) < 0.9f;
+    if (depth_miss || normal_miss || instance_miss) {
+        r = zero_reservoir();
+        return false;
+    }
+    return true;
+}
+HKD void temporal_restir(Reservoir& r, const Sample& s, float w_new, uint32_t max_sample_count)
+{
+    update_reservoir(r, s, w_new);
+    float m = (float)max_sample_count;
+    if (r.count > m) {
+        r.w_sum *= m / r.count;
+        r.w2_sum *= m / r.count;
+        r.count = m;
+    }
+}
+HKD float variance_of(const Reservoir& r)
+{
+    float variance = r.w2_sum / r.count - hk_pow(r.w_sum / r.count, 2.0f);
+    variance = r.count < 1.0f ? variance : variance / r.count;
+    return fminf(variance, MAX_VARIANCE);
+}
+
+// ------------------------------------------------------------------ tracing (light.wgsl:259-533)
+struct Ray {
+    f3 origin, direction, inv_direction;
+};
+struct Hit {
+    f2 uv;
+    float distance;
+    uint32_t instance_index, primitive_index;
+};
+struct HitInfo {
+    f4 position;
+    f3 normal;
+    f2 uv;
+    uint32_t instance_index, material_index;
+};
+struct LightCandidate {
+    f3 direction;
+    float max_distance, min_distance;
+    uint32_t emissive_instance;
+    float p;
+};
+struct Surface {
+    f4 base_color, emissive;
+    float reflectance, metallic, roughness, occlusion;
+};
+
+HKD float intersects_aabb(const Ray& ray, f3 mn, f3 mx)
+{
+    f3 t1 = (mn - ray.origin) * ray.inv_direction;
+    f3 t2 = (mx - ray.origin) * ray.inv_direction;
+    float t_min = fminf(t1.x, t2.x);
+    float t_max = fmaxf(t1.x, t2.x);
+    t_min = fmaxf(t_min, fminf(t1.y, t2.y));
+    t_max = fminf(t_max, fmaxf(t1.y, t2.y));
+    t_min = fmaxf(t_min, fminf(t1.z, t2.z));
+    t_max = fminf(t_max, fmaxf(t1.z, t2.z));
+    return (t_max >= t_min && t_max >= 0.0f) ? t_min : HK_F32_MAX;
+}
+
+// Möller–Trumbore as light.wgsl:364-398; returns distance (F32_MAX on miss) and uv.
+HKD float intersects_triangle(const Ray& ray, f3 p0, f3 p1, f3 p2, f2& uv_out)
+{
+    uv_out = mk2(0.0f, 0.0f);
+    f3 ab = p1 - p0;
+    f3 ac = p2 - p0;
+    f3 u_vec = cross(ray.direction, ac);
+    float det = dot(ab, u_vec);
+    if (fabsf(det) < HK_F32_EPSILON) return HK_F32_MAX;
+    float inv_det = 1.0f / det;
+    f3 ao = ray.origin - p0;
+    float u = dot(ao, u_vec) * inv_det;
+    if (u < 0.0f || u > 1.0f) {
+        uv_out = mk2(u, 0.0f);
+        return HK_F32_MAX;
+    }
+    f3 v_vec = cross(ao, ab);
+    float v = dot(ray.direction, v_vec) * inv_det;
+    uv_out = mk2(u, v);
+    if (v < 0.0f || u + v > 1.0f) return HK_F32_MAX;
+    float distance = dot(ac, v_vec) * inv_det;
+    return distance > HK_F32_EPSILON ? distance : HK_F32_MAX;
+}
+
+HKD void load_node(const hk_node* nodes, uint32_t i, f3& mn, uint32_t& entry, f3& mx, uint32_t& exit)
+{
+    const float4* p = reinterpret_cast<const float4*>(nodes + i);
+    float4 a = p[0], b = p[1];
+    mn = mk3(a.x, a.y, a.z);
+    entry = __float_as_uint(a.w);
+    mx = mk3(b.x, b.y, b.z);
+    exit = __float_as_uint(b.w);
+}
+HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& c)
+{
+    const float4* p = reinterpret_cast<const float4*>(prims + i);
+    float4 x = p[0], y = p[1], z = p[2];
+    a = mk3(x.x, x.y, x.z);
+    b = mk3(y.x, y.y, y.z);
+    c = mk3(z.x, z.y, z.z);
+}
+
+// light.wgsl:400-440 — stackless skip-pointer BLAS walk (reference visit order).
+HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t node_offset, uint32_t node_count,
+                         uint32_t prim_offset, float early_distance)
+{
+    bool intersected = false;
+    uint32_t index = 0u;
+    while (index < node_count) {
+        f3 mn, mx;
+        uint32_t entry, exit;
+        load_node(sc.asset_nodes, node_offset + index, mn, entry, mx, exit);
+        if (entry >= HK_BVH_LEAF_FLAG) {
+            uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
+            f3 a, b, c;
+            load_triangle(sc.primitives, primitive_index, a, b, c);
+            f3 tmn = vmin(a, vmin(b, c));
+            f3 tmx = vmax(a, vmax(b, c));
+            if (intersects_aabb(ray, tmn, tmx) < hit.distance) {
+                f2 uv;
+                float d = intersects_triangle(ray, a, b, c, uv);
+                if (d < hit.distance) {
+                    hit.distance = d;
+                    hit.uv = uv;
+                    hit.primitive_index = primitive_index;
+                    intersected = true;
+                    if (d < early_distance) return intersected;
+                }
+            }
+            index = exit;
+        } else {
+            index = intersects_aabb(ray, mn, mx) < hit.distance ? entry : exit;
+        }
+    }
+    return intersected;
+}
+
+HKD f3 world_to_local_point(const hk_instance& in, f3 p)
+{
+    const float* m = in.inverse_transpose_model;  // inverse_model = transpose(itm)
+    float x = ((m[0] * p.x + m[1] * p.y) + m[2] * p.z) + m[3] * 1.0f;
+    float y = ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7] * 1.0f;
+    float z = ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11] * 1.0f;
+    float w = ((m[12] * p.x + m[13] * p.y) + m[14] * p.z) + m[15] * 1.0f;
+    return mk3(x / w, y / w, z / w);
+}
+HKD f3 world_to_local_dir(const hk_instance& in, f3 p)
+{
+    const float* m = in.inverse_transpose_model;
+    float x = ((m[0] * p.x + m[1] * p.y) + m[2] * p.z) + m[3] * 0.0f;
+    float y = ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7] * 0.0f;
+    float z = ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11] * 0.0f;
+    return mk3(x, y, z);
+}
+HKD f3 local_to_world_point(const hk_instance& in, f3 p)
+{
+    f4 r = mat4_mul(in.model, mk4(p.x, p.y, p.z, 1.0f));
+    return mk3(r.x / r.w, r.y / r.w, r.z / r.w);
+}
+HKD f3 local_to_world_normal(const hk_instance& in, f3 n)
+{
+    const float* m = in.inverse_transpose_model;
+    f3 r;
+    r.x = (m[0] * n.x + m[4] * n.y) + m[8] * n.z;
+    r.y = (m[1] * n.x + m[5] * n.y) + m[9] * n.z;
+    r.z = (m[2] * n.x + m[6] * n.y) + m[10] * n.z;
+    return normalize(r);
+}
+
+// light.wgsl:442-486 — stackless skip-pointer TLAS walk.
+HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float early_distance, uint32_t exclude)
+{
+    Hit hit;
+    hit.uv = mk2(0.0f, 0.0f);
+    hit.distance = max_distance;
+    hit.instance_index = HK_U32_MAX;
+    hit.primitive_index = HK_U32_MAX;
+    uint32_t index = 0u;
+    while (index < sc.n_instance_nodes) {
+        f3 mn, mx;
+        uint32_t entry, exit;
+        load_node(sc.instance_nodes, index, mn, entry, mx, exit);
+        if (entry >= HK_BVH_LEAF_FLAG) {
+            uint32_t instance_index = entry - HK_BVH_LEAF_FLAG;
+            const hk_instance& in = sc.instances[instance_index];
+            if (instance_index != exclude && intersects_aabb(ray, ld3(in.min), ld3(in.max)) < hit.distance) {
+                Ray r;
+                r.origin = world_to_local_point(in, ray.origin);
+                r.direction = world_to_local_dir(in, ray.direction);
+                r.inv_direction = inv(r.direction);
+                if (traverse_bottom(sc, hit, r, in.mesh.node[0], in.mesh.node[1], in.mesh.primitive, early_distance)) {
+                    hit.instance_index = instance_index;
+                    if (hit.distance < early_distance) return hit;
+                }
+            }
+            index = exit;
+        } else {
+            index = intersects_aabb(ray, mn, mx) < hit.distance ? entry : exit;
+        }
+    }
+    return hit;
+}
+
+HKD const hk_instance& get_instance(const Scene& sc, uint32_t i) { return sc.instances[i < sc.n_instances ? i : sc.n_instances - 1]; }
+HKD const hk_material& get_material(const Scene& sc, uint32_t i) { return sc.materials[i < sc.n_materials ? i : sc.n_materials - 1]; }
+
+HKD HitInfo empty_hit_info(f3 position, f3 direction)
+{
+    HitInfo info;
+    info.instance_index = HK_U32_MAX;
+    info.material_index = HK_U32_MAX;
+    f3 p = position + direction * DISTANCE_MAX;
+    info.position = mk4(p.x, p.y, p.z, 0.0f);
+    info.normal = mk3(0, 0, 0);
+    info.uv = mk2(0, 0);
+    return info;
+}
+HKD HitInfo hit_info(const Scene& sc, const Ray& ray, const Hit& hit)
+{
+    HitInfo info;
+    info.instance_index = hit.instance_index;
+    info.material_index = HK_U32_MAX;
+    info.normal = mk3(0, 0, 0);
+    info.uv = mk2(0, 0);
+    if (hit.instance_index != HK_U32_MAX) {
+        const hk_instance& in = get_instance(sc, hit.instance_index);
+        const hk_primitive& pr = sc.primitives[hit.primitive_index];
+        const hk_vertex& v0 = sc.vertices[in.mesh.vertex + pr.vertices[0].index];
+        const hk_vertex& v1 = sc.vertices[in.mesh.vertex + pr.vertices[1].index];
+        const hk_vertex& v2 = sc.vertices[in.mesh.vertex + pr.vertices[2].index];
+        f2 uv = hit.uv;
+        info.uv = mk2((v0.u + uv.x * (v1.u - v0.u)) + uv.y * (v2.u - v0.u),
+                      (v0.v + uv.x * (v1.v - v0.v)) + uv.y * (v2.v - v0.v));
+        f3 n0 = ld3(v0.normal), n1 = ld3(v1.normal), n2 = ld3(v2.normal);
+        f3 n = (n0 + (n1 - n0) * uv.x) + (n2 - n0) * uv.y;
+        info.normal = local_to_world_normal(in, n);
+        f3 p = ray.origin + ray.direction * hit.distance;
+        info.position = mk4(p.x, p.y, p.z, 1.0f);
+        info.material_index = in.material;
+    } else {
+        f3 p = ray.origin + ray.direction * DISTANCE_MAX;
+        info.position = mk4(p.x, p.y, p.z, 0.0f);
+    }
+    return info;
+}
+HKD void occlude_hit_info(const Ray& ray, const Hit& hit, HitInfo& info)
+{
+    if (hit.instance_index != HK_U32_MAX) {
+        info.instance_index = hit.instance_index;
+        info.material_index = HK_U32_MAX;
+        f3 p = ray.origin + ray.direction * hit.distance;
+        info.position = mk4(p.x, p.y, p.z, 1.0f);
+        info.normal = mk3(0, 0, 0);
+    }
+}
+
+// ------------------------------------------------------------------ sampling (light.wgsl:537-708)
+HKD f4 sample_cosine_hemisphere(f2 rand)
+{
+    float r = sqrtf(rand.x);
+    float theta = (2.0f * HK_PI) * rand.y;
+    float sn, cs;
+    hk_sincos(theta, &sn, &cs);
+    f2 t = mk2(r * cs, r * sn);
+    float z = sqrtf(1.0f - dot(t, t));
+    return mk4(t.x, t.y, z, (2.0f * HK_INV_TAU) * z);
+}
+HKD f4 sample_uniform_cone(f2 rand, float cos_angle)
+{
+    float z = 1.0f - (1.0f - cos_angle) * rand.x;
+    float theta = HK_TAU * rand.y;
+    float r = sqrtf(1.0f - z * z);
+    float sn, cs;
+    hk_sincos(theta, &sn, &cs);
+    return mk4(r * cs, r * sn, z, HK_INV_TAU / (1.0f - cos_angle));
+}
+HKD void normal_basis(f3 n, f3& t, f3& b)
+{
+    float sg = n.z > 0.0f ? 1.0f : (n.z < 0.0f ? -1.0f : 0.0f);
+    float s = fminf(sg * 2.0f + 1.0f, 1.0f);
+    float u = -1.0f / (s + n.z);
+    float v = (n.x * n.y) * u;
+    t = mk3(1.0f + ((s * n.x) * n.x) * u, s * v, -s * n.x);
+    b = mk3(v, s + (n.y * n.y) * u, -n.y);
+}
+HKD f3 basis_mul(f3 t, f3 b, f3 n, f3 d) { return (t * d.x + b * d.y) + n * d.z; }
+HKD f3 emissive_radiance(f4 e) { return xyz(e) * (255.0f * e.w); }
+
+template <bool COUNT>
+HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 rand, f3 position, f3 normal,
+                                          uint32_t instance, HitInfo& info, uint32_t& n_emitter)
+{
+    LightCandidate candidate;
+    candidate.max_distance = HK_F32_MAX;
+    candidate.min_distance = DISTANCE_MAX;
+    candidate.emissive_instance = DONT_SAMPLE_EMISSIVE;
+    f3 cone = ld3(F.direction_to_light);
+    f3 bt, bb;
+    normal_basis(cone, bt, bb);
+    f3 rand_direction = basis_mul(bt, bb, cone, xyz(sample_uniform_cone(mk2(rand.z, rand.w), F.cos_solar_angle)));
+    candidate.direction = rand_direction;
+    candidate.p = 1.0f;
+    info = empty_hit_info(position, rand_direction);
+    if (instance == DONT_SAMPLE_EMISSIVE) return candidate;
+
+    uint32_t picked = 0u;
+    float count = 0.0f;
+    uint32_t index = 0u;
+    float rand_1d = rand.x;
+    while (index < sc.n_emissive_nodes) {
+        f3 mn, mx;
+        uint32_t entry, exit;
+        load_node(sc.emissive_nodes, index, mn, entry, mx, exit);
+        if (entry >= HK_BVH_LEAF_FLAG) {
+            uint32_t ei = entry - HK_BVH_LEAF_FLAG;
+            const hk_emissive& cur = sc.emissives[ei];
+            f3 ep = ld3(cur.position);
+            float rad = cur.radius;
+            f3 emn = mk3(ep.x - rad, ep.y - rad, ep.z - rad), emx = mk3(ep.x + rad, ep.y + rad, ep.z + rad);
+            bool inside = (position.x > emn.x && position.y > emn.y && position.z > emn.z) &&
+                          (position.x < emx.x && position.y < emx.y && position.z < emx.z);
+            if (instance != cur.instance && inside) {
+                rand_1d = hk_fract(rand_1d + HK_GOLDEN_RATIO);
+                count += 1.0f;
+                if (rand_1d < 1.0f / count) {
+                    candidate.emissive_instance = cur.instance;
+                    picked = ei;
+                }
+            }
+            index = exit;
+        } else {
+            bool inside = (position.x > mn.x && position.y > mn.y && position.z > mn.z) &&
+                          (position.x < mx.x && position.y < mx.y && position.z < mx.z);
+            index = inside ? entry : exit;
+        }
+    }
+    if (candidate.emissive_instance != DONT_SAMPLE_EMISSIVE) {
+        const hk_emissive& emissive = sc.emissives[picked];
+        uint32_t len = emissive.alias_table[1];
+        uint32_t alias_index = f2u32(rand.x * (float)len);
+        if (alias_index > len - 1u) alias_index = len - 1u;
+        hk_alias_entry ae = sc.alias_table[emissive.alias_table[0] + alias_index];
+        uint32_t primitive_index = rand.y < ae.prob ? ae.index : alias_index;
+        const hk_instance& ein = get_instance(sc, candidate.emissive_instance);
+        f3 v0, v1, v2;
+        load_triangle(sc.primitives, ein.mesh.primitive + primitive_index, v0, v1, v2);
+        float srx = sqrtf(rand.z);
+        f2 b = mk2(1.0f - srx, rand.w * srx);
+        f3 p = local_to_world_point(ein, (v0 * b.x + v1 * b.y) + v2 * ((1.0f - b.x) - b.y));
+
+        Hit hit;
+        hit.uv = mk2(0, 0);
+        hit.distance = HK_F32_MAX;
+        hit.instance_index = HK_U32_MAX;
+        hit.primitive_index = HK_U32_MAX;
+        Ray ray;
+        ray.origin = position + normal * RAY_BIAS;
+        ray.direction = normalize(p - position);
+        ray.inv_direction = mk3(0, 0, 0);
+        Ray r;
+        r.origin = world_to_local_point(ein, ray.origin);
+        r.direction = world_to_local_dir(ein, ray.direction);
+        r.inv_direction = inv(r.direction);
+        candidate.direction = ray.direction;
+        bool traced = false;
+        if (dot(candidate.direction, normal) > 0.0f) {
+            if (COUNT) n_emitter++;
+            traced = traverse_bottom(sc, hit, r, ein.mesh.node[0], ein.mesh.node[1], ein.mesh.primitive, 0.0f);
+        }
+        if (traced) {
+            hit.instance_index = emissive.instance;
+            info = hit_info(sc, ray, hit);
+            candidate.max_distance = hit.distance;
+            candidate.min_distance = hit.distance - 0.1f;
+            f3 delta = xyz(info.position) - position;
+            candidate.p = dot(delta, delta) / fabsf(dot(ray.direction, info.normal) * emissive.surface_area);
+            candidate.p = candidate.p / count;
+        } else {
+            info = empty_hit_info(ray.origin, ray.direction);
+            candidate.emissive_instance = DONT_SAMPLE_EMISSIVE;
+            candidate.direction = rand_direction;
+            candidate.p = 1.0f;
+        }
+    }
+    return candidate;
+}
+
+// ------------------------------------------------------------------ shading (light.wgsl:714-908 + Bevy PBR)
+HKD f3 calculate_view(const Frame& F, f4 world_position)
+{
+    if (F.orthographic) return normalize(ld3(F.view_proj_z));
+    return normalize(ld3(F.view_world_position) - xyz(world_position));
+}
+HKD Surface retreive_surface(const Scene& sc, uint32_t material_index)
+{
+    const hk_material& m = get_material(sc, material_index);
+    Surface s;
+    s.base_color = mk4(m.base_color[0], m.base_color[1], m.base_color[2], m.base_color[3]);
+    s.emissive = mk4(m.emissive[0], m.emissive[1], m.emissive[2], m.emissive[3]);
+    s.metallic = m.metallic;
+    s.occlusion = 1.0f;
+    float pr = hk_clampf(m.perceptual_roughness, 0.089f, 1.0f);
+    s.roughness = pr * pr;
+    s.reflectance = m.reflectance;
+    return s;
+}
+HKD f4 retreive_emissive(const Scene& sc, uint32_t material_index)
+{
+    const hk_material& m = get_material(sc, material_index);
+    return mk4(m.emissive[0], m.emissive[1], m.emissive[2], m.emissive[3]);
+}
+HKD float F_Schlick(float f0, float f90, float VoH) { return f0 + (f90 - f0) * hk_pow(1.0f - VoH, 5.0f); }
+HKD f3 F_Schlick_vec(f3 f0, float f90, float VoH)
+{
+    float k = hk_pow(1.0f - VoH, 5.0f);
+    return mk3(f0.x + (f90 - f0.x) * k, f0.y + (f90 - f0.y) * k, f0.z + (f90 - f0.z) * k);
+}
+HKD f3 EnvBRDFApprox(f3 f0, float pr, float NoV)
+{
+    float rx = pr * -1.0f + 1.0f;
+    float ry = pr * -0.0275f + 0.0425f;
+    float rz = pr * -0.572f + 1.04f;
+    float rw = pr * 0.022f + -0.04f;
+    float a004 = fminf(rx * rx, hk_exp2(-9.28f * NoV)) * rx + ry;
+    float ABx = -1.04f * a004 + rz;
+    float ABy = 1.04f * a004 + rw;
+    return mk3(f0.x * ABx + ABy, f0.y * ABx + ABy, f0.z * ABx + ABy);
+}
+HKD f3 lit(f3 radiance, f3 diffuse_color, float roughness, f3 F0, f3 L, f3 N, f3 V)
+{
+    f3 H = normalize(L + V);
+    float NoL = hk_saturate(dot(N, L));
+    float NoH = hk_saturate(dot(N, H));
+    float LoH = hk_saturate(dot(L, H));
+    float NdotV = fmaxf(dot(N, V), 0.0001f);
+    // Fd_Burley
+    float f90 = 0.5f + ((2.0f * roughness) * LoH) * LoH;
+    float fd = (F_Schlick(1.0f, f90, NoL) * F_Schlick(1.0f, f90, NdotV)) * (1.0f / HK_PI);
+    f3 diffuse = diffuse_color * fd;
+    // specular = D_GGX * V_SmithGGXCorrelated * fresnel
+    float one_minus = 1.0f - NoH * NoH;
+    float a = NoH * roughness;
+    float k = roughness / (one_minus + a * a);
+    float D = (k * k) * (1.0f / HK_PI);
+    float a2 = roughness * roughness;
+    float lambdaV = NoL * sqrtf((NdotV - a2 * NdotV) * NdotV + a2);
+    float lambdaL = NdotV * sqrtf((NoL - a2 * NoL) * NoL + a2);
+    float Vis = 0.5f / (lambdaV + lambdaL);
+    float fr90 = hk_saturate(dot(F0, mk3(16.5f, 16.5f, 16.5f)));
+    f3 F = F_Schlick_vec(F0, fr90, LoH);
+    f3 specular_light = F * ((1.0f * D) * Vis);
+    return ((specular_light + diffuse) * radiance) * NoL;
+}
+HKD f3 ambient(const Frame& F, f3 diffuse_color, float roughness, float occlusion, f3 F0, f3 N, f3 V)
+{
+    float NdotV = fmaxf(dot(N, V), 0.0001f);
+    f3 da = EnvBRDFApprox(diffuse_color, 1.0f, NdotV);
+    f3 sa = EnvBRDFApprox(F0, roughness, NdotV);
+    return ((da + sa) * occlusion) * ld3(F.ambient_color);
+}
+HKD f4 input_radiance(const Scene& sc, const Frame& F, const Ray& ray, const HitInfo& info, bool sample_directional,
+                      uint32_t sample_emissive, bool sample_ambient)
+{
+    f3 radiance = mk3(0, 0, 0);
+    float amb = 0.0f;
+    if (info.instance_index == HK_U32_MAX) {
+        bool hit_directional = dot(ray.direction, ld3(F.direction_to_light)) >= F.cos_solar_angle;
+        if (sample_directional && hit_directional) {
+            radiance = ld3(F.directional_color);
+            amb = 0.0f;
+        } else {
+            radiance = sample_ambient ? ld3(F.ambient_color) : mk3(0, 0, 0);
+            amb = 1.0f;
+        }
+    } else if (sample_emissive == info.instance_index) {
+        radiance = emissive_radiance(retreive_emissive(sc, info.material_index));
+    }
+    return mk4(radiance.x, radiance.y, radiance.z, 1.0f - amb);
+}
+HKD f3 shading(const Frame& F, f3 V, f3 N, f3 L, const Surface& s, f4 in_radiance)
+{
+    f3 base = xyz(s.base_color);
+    float f0s = ((0.16f * s.reflectance) * s.reflectance) * (1.0f - s.metallic);
+    f3 F0 = mk3(f0s + base.x * s.metallic, f0s + base.y * s.metallic, f0s + base.z * s.metallic);
+    f3 diffuse_color = base * (1.0f - s.metallic);
+    f3 lr = lit(xyz(in_radiance), diffuse_color, s.roughness, F0, L, N, V);
+    f3 ar = ambient(F, diffuse_color, s.roughness, s.occlusion, F0, N, V);
+    return mix(lr, ar, 1.0f - in_radiance.w);
+}
+HKD f3 env_brdf(f3 V, f3 N, const Surface& s)
+{
+    f3 base = xyz(s.base_color);
+    float NdotV = fmaxf(dot(N, V), 0.0001f);
+    float f0s = ((0.16f * s.reflectance) * s.reflectance) * (1.0f - s.metallic);
+    f3 F0 = mk3(f0s + base.x * s.metallic, f0s + base.y * s.metallic, f0s + base.z * s.metallic);
+    f3 diffuse_color = base * (1.0f - s.metallic);
+    return (EnvBRDFApprox(diffuse_color, 1.0f, NdotV) + EnvBRDFApprox(F0, s.roughness, NdotV)) * s.occlusion;
+}
+HKD float compute_jacobian(const Sample& q, const Sample& r)
+{
+    f3 normal = q.sample_normal;
+    float c1 = fabsf(dot(normalize(xyz(r.visible_position) - xyz(q.sample_position)), normal));
+    float c2 = fabsf(dot(normalize(xyz(q.visible_position) - xyz(q.sample_position)), normal));
+    float term_1 = c1 / fmaxf(0.0001f, c2);
+    float num = length(xyz(q.visible_position) - xyz(q.sample_position));
+    num *= num;
+    float denom = length(xyz(r.visible_position) - xyz(q.sample_position));
+    denom *= denom;
+    float term_2 = num / fmaxf(denom, 0.0001f);
+    return hk_clampf(term_1 * term_2, 1.0f, 50.0f);
+}
+
+// blue noise (light.wgsl:1075-1079): nearest + repeat => texel ((x + n) & 63, (y + n) & 63)
+HKD f4 noise_random(const uchar4* noise, uint32_t number, int32_t x, int32_t y)
+{
+    uint32_t id = number & 15u;
+    uint32_t tx = ((uint32_t)x + number) & 63u, ty = ((uint32_t)y + number) & 63u;
+    uchar4 t = noise[(id * 64u + ty) * 64u + tx];
+    float fn = (float)number * HK_GOLDEN_RATIO;
+    return mk4(hk_fract((float)t.x / 255.0f + fn), hk_fract((float)t.y / 255.0f + fn), hk_fract((float)t.z / 255.0f + fn),
+               hk_fract((float)t.w / 255.0f + fn));
+}
+
+// wave-aggregated 64-bit counter add (one atomic per wave)
+HKD void wave_count(unsigned long long* dst, uint32_t v)
+{
+    unsigned long long s = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
+}
+
+}  // namespace hk

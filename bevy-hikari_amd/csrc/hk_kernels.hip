@@ -1,0 +1,751 @@
+// hk_kernels.hip — gfx950 kernels of the integrator and denoiser.
+//
+// Entry point map (reference -> kernel):
+//   light.wgsl:1019 full_screen_albedo          -> k_albedo
+//   light.wgsl:1044 direct_lit (+RENDER_EMISSIVE / +EMISSIVE_LIT) -> k_direct<EMISSIVE_LIT, RENDER_EMISSIVE>
+//   light.wgsl:1263 indirect_lit_ambient (+MULTIPLE_BOUNCES)      -> k_indirect<MULTI>
+//   light.wgsl:1503 spatial_reuse (+EMISSIVE_LIT)                 -> k_spatial<EMISSIVE_LIT>
+//   denoise.wgsl:135 demodulation                                 -> k_demod
+//   denoise.wgsl:215 denoise (DENOISE_LEVEL_0..3, FIREFLY)        -> k_denoise<FIREFLY>
+//   tone_mapping.wgsl:21 tone_mapping                             -> k_tone
+//   prepass.wgsl:84-100 (raster G-buffer)                         -> k_gbuffer (primary rays)
+//   light.wgsl:442 traverse_top                                   -> k_trace
+//
+// Launch shape: 256-thread workgroups covering a 16x16 pixel tile, each wave an 8x8
+// sub-tile (the reference's workgroup footprint), so rays of one wave stay coherent.
+#include "hk_device.h"
+#include "hk_launch.h"
+
+namespace hk {
+
+// workgroup tile -> pixel (global coordinates)
+HKD bool tile_pixel(uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
+{
+    uint32_t t = threadIdx.x;
+    uint32_t w = t >> 6, lane = t & 63u;
+    x = (int32_t)(blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u));
+    int32_t ly = (int32_t)(blockIdx.y * 16u + (w >> 1) * 8u + (lane >> 3));
+    y = row0 + ly;
+    return (uint32_t)x < width && ly < rows;
+}
+
+// ------------------------------------------------------------------ G-buffer
+HKD f3 primary_direction(const ViewArgs& V, float px, float py, const uint32_t* size)
+{
+    float ndc_x = (px / (float)size[0]) * 2.0f - 1.0f;
+    float ndc_y = 1.0f - (py / (float)size[1]) * 2.0f;
+    f4 p = mat4_mul(V.inverse_view_proj, mk4(ndc_x, ndc_y, 1.0f, 1.0f));
+    f3 nearp = mk3(p.x / p.w, p.y / p.w, p.z / p.w);
+    return normalize(nearp - ld3(V.world_position));
+}
+HKD float ndc_depth(const float* vp, f3 p)
+{
+    f4 c = mat4_mul(vp, mk4(p.x, p.y, p.z, 1.0f));
+    return c.z / c.w;
+}
+
+__global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V)
+{
+    int32_t x, y;
+    bool active = tile_pixel(A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
+    uint32_t n_primary = 0;
+    if (active) {
+        n_primary = 1;
+        int32_t idx = x + (int32_t)A.F.S[0] * (y - A.F.S_row0);
+        Ray ray;
+        ray.origin = ld3(V.world_position);
+        ray.direction = primary_direction(V, (float)x + 0.5f, (float)y + 0.5f, A.F.S);
+        ray.inv_direction = inv(ray.direction);
+        Hit hit = traverse_top(A.sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+        if (hit.instance_index == HK_U32_MAX) {
+            A.G.position[idx] = make_float4(0, 0, 0, 0);
+            A.G.normal[idx] = 0u;
+            A.G.depth_gradient[idx] = make_float2(0, 0);
+            A.G.instance_material[idx] = make_float2(0, 0);
+            A.G.velocity_uv[idx] = make_float4(0, 0, 0, 0);
+        } else {
+            HitInfo info = hit_info(A.sc, ray, hit);
+            f3 p = xyz(info.position);
+            float depth = ndc_depth(V.view_proj, p);
+            A.G.position[idx] = make_float4(p.x, p.y, p.z, depth);
+            A.G.normal[idx] = hk_pack4x8snorm(info.normal.x, info.normal.y, info.normal.z, 1.0f);
+            const hk_instance& in = get_instance(A.sc, hit.instance_index);
+            f3 t0, t1, t2;
+            load_triangle(A.sc.primitives, hit.primitive_index, t0, t1, t2);
+            f3 w0 = local_to_world_point(in, t0), w1 = local_to_world_point(in, t1), w2 = local_to_world_point(in, t2);
+            f3 ng = cross(w1 - w0, w2 - w0);
+            float plane = dot(p - ray.origin, ng);
+            float grad[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                f3 d = primary_direction(V, (float)x + 0.5f + (k == 0 ? 1.0f : 0.0f),
+                                         (float)y + 0.5f + (k == 1 ? 1.0f : 0.0f), A.F.S);
+                float denom = dot(d, ng);
+                grad[k] = 0.0f;
+                if (denom != 0.0f) {
+                    float t = plane / denom;
+                    grad[k] = ndc_depth(V.view_proj, ray.origin + d * t) - depth;
+                }
+            }
+            A.G.depth_gradient[idx] = make_float2(grad[0], grad[1]);
+            A.G.instance_material[idx] = make_float2((float)hit.instance_index + 0.5f, (float)info.material_index + 0.5f);
+            A.G.velocity_uv[idx] = make_float4(0.0f, 0.0f, info.uv.x, info.uv.y);
+        }
+    }
+    wave_count(A.cnt.primary, n_primary);
+}
+
+// ------------------------------------------------------------------ albedo (light.wgsl:1019-1042)
+__global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
+{
+    int32_t x, y;
+    if (!tile_pixel(A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
+    int32_t idx = x + (int32_t)A.F.S[0] * (y - A.F.S_row0);
+    f4 pd = load_position(A.F, A.G, x, y);
+    if (pd.w < HK_F32_EPSILON) {
+        store_rgba16f(albedo, idx, mk4(0, 0, 0, 0));
+        return;
+    }
+    f3 normal = load_normal(A.F, A.G, x, y);
+    uint32_t material = f2u32(load_instance_material(A.F, A.G, x, y).y);
+    Surface surface = retreive_surface(A.sc, material);
+    f3 view_direction = calculate_view(A.F, mk4(pd.x, pd.y, pd.z, 1.0f));
+    f3 a = env_brdf(view_direction, normal, surface);
+    store_rgba16f(albedo, idx, mk4(a.x, a.y, a.z, 1.0f));
+}
+
+// ------------------------------------------------------------------ direct_lit (light.wgsl:1044-1261)
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE>
+HKD void direct_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top, uint32_t& n_emitter)
+{
+    const Frame& F = A.F;
+    const int32_t idx = s_index(F, x, y);
+    const f2 uv = coords_to_uv(x, y, F.s);
+    int32_t dx, dy;
+    jittered_coords(F, uv, dx, dy);
+    f4 pd = load_position(F, A.G, dx, dy);
+    f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
+    float depth = pd.w;
+    Sample s = zero_sample();
+    if (depth < HK_F32_EPSILON) {
+        Reservoir r = zero_reservoir();
+        set_reservoir(r, s, 0.0f);
+        store_res(C.cur, idx, r);
+        store_res(C.spatial, idx, r);
+        store_res(C.prev_spatial, idx, r);
+        C.variance[idx] = 0.0f;
+        store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
+        return;
+    }
+    f3 normal = load_normal(F, A.G, dx, dy);
+    f2 imf = load_instance_material(F, A.G, dx, dy);
+    uint32_t im_x = f2u32(imf.x), im_y = f2u32(imf.y);
+    f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
+
+    s.random = noise_random(A.noise, F.number, x, y);
+    s.visible_position = mk4(position.x, position.y, position.z, depth);
+    s.visible_normal = normal;
+    s.visible_instance = im_x;
+
+    Ray ray;
+    ray.origin = ray.direction = ray.inv_direction = mk3(0, 0, 0);
+    HitInfo info = empty_hit_info(mk3(0, 0, 0), mk3(0, 0, 0));
+
+    f2 juv = jittered_uv(F, uv, 0.25f);
+    f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
+    Reservoir r = load_previous(F, C.prev, previous_uv);
+    if (!check_previous_reservoir(r, s) && uv_inside_closed(previous_uv)) {
+        int32_t px = f2i32(previous_uv.x * (float)F.s[0]);
+        int32_t py = f2i32(previous_uv.y * (float)F.s[1]);
+        store_res(C.prev_spatial, s_index(F, px, py), r);
+    }
+
+    const uint32_t validate_interval = EMISSIVE_LIT ? F.emissive_validate_interval : F.direct_validate_interval;
+    const uint32_t select_light_instance = EMISSIVE_LIT ? im_x : DONT_SAMPLE_EMISSIVE;
+
+    if (umod(F.number, validate_interval) != 0u || r.count < 4.0f) {
+        LightCandidate cand = select_light_candidate<true>(A.sc, F, s.random, xyz(s.visible_position), s.visible_normal,
+                                                           select_light_instance, info, n_emitter);
+        ray.origin = xyz(position) + normal * RAY_BIAS;
+        ray.direction = cand.direction;
+        ray.inv_direction = inv(ray.direction);
+        bool trace = dot(cand.direction, normal) > 0.0f && cand.p > 0.0f;
+        if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
+        if (trace) {
+            n_top++;
+            Hit hit = traverse_top(A.sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
+            occlude_hit_info(ray, hit, info);
+            s.radiance = EMISSIVE_LIT ? input_radiance(A.sc, F, ray, info, false, cand.emissive_instance, false)
+                                      : input_radiance(A.sc, F, ray, info, true, DONT_SAMPLE_EMISSIVE, false);
+        }
+        s.sample_position = info.position;
+        s.sample_normal = info.normal;
+        float w_new = cand.p > 0.0f ? lum(xyz(s.radiance)) / cand.p : 0.0f;
+        temporal_restir(r, s, w_new, F.max_temporal_reuse_count);
+    }
+
+    if (umod(F.number, validate_interval) == 0u) {
+        LightCandidate cand = select_light_candidate<true>(A.sc, F, r.s.random, xyz(r.s.visible_position),
+                                                           r.s.visible_normal, select_light_instance, info, n_emitter);
+        ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
+        ray.direction = normalize(xyz(r.s.sample_position) - xyz(s.visible_position));
+        ray.inv_direction = inv(ray.direction);
+        f4 validate_radiance = mk4(0, 0, 0, 0);
+        bool trace = dot(cand.direction, r.s.visible_normal) > 0.0f && cand.p > 0.0f;
+        if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
+        if (trace) {
+            n_top++;
+            Hit hit = traverse_top(A.sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
+            occlude_hit_info(ray, hit, info);
+            validate_radiance = EMISSIVE_LIT ? input_radiance(A.sc, F, ray, info, false, cand.emissive_instance, false)
+                                             : input_radiance(A.sc, F, ray, info, true, DONT_SAMPLE_EMISSIVE, false);
+        }
+        if (r.count >= 4.0f) {
+            s.random = r.s.random;
+            s.sample_position = info.position;
+            s.sample_normal = info.normal;
+            s.radiance = validate_radiance;
+        }
+        float ratio = lum(xyz(validate_radiance)) / fmaxf(lum(xyz(r.s.radiance)), 0.0001f);
+        if (ratio > 1.25f || ratio < 0.8f) {
+            if (uv_inside_closed(previous_uv)) {
+                int32_t px = f2i32(previous_uv.x * (float)F.s[0]);
+                int32_t py = f2i32(previous_uv.y * (float)F.s[1]);
+                store_res(C.prev_spatial, s_index(F, px, py), r);
+            }
+            float w_new = cand.p > 0.0f ? lum(xyz(s.radiance)) / cand.p : 0.0f;
+            set_reservoir(r, s, w_new);
+        }
+    }
+
+    float total_lum = r.count * lum(xyz(r.s.radiance));
+    r.w = total_lum > 0.0f ? r.w_sum / total_lum : 0.0f;
+    r.s.visible_position = s.visible_position;
+    r.s.visible_normal = s.visible_normal;
+    r.lifetime += 1.0f;
+    C.variance[idx] = variance_of(r);
+    if (F.temporal_reuse > 0u) store_res(C.cur, idx, r);
+
+    Surface surface = retreive_surface(A.sc, im_y);
+    f3 view_direction = calculate_view(F, position);
+    f3 out = shading(F, view_direction, r.s.visible_normal, normalize(xyz(r.s.sample_position) - xyz(r.s.visible_position)),
+                     surface, r.s.radiance);
+    out = out * r.w;
+    if (RENDER_EMISSIVE) out = out + emissive_radiance(surface.emissive);
+    store_rgba16f(C.render, idx, mk4(out.x, out.y, out.z, 1.0f));
+}
+
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE>
+__global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
+{
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+        direct_body<EMISSIVE_LIT, RENDER_EMISSIVE>(A, C, x, y, n_top, n_emitter);
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
+// ------------------------------------------------------------------ indirect_lit_ambient (light.wgsl:1263-1498)
+template <bool MULTI>
+HKD void indirect_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top, uint32_t& n_emitter)
+{
+    const Frame& F = A.F;
+    const int32_t idx = s_index(F, x, y);
+    const f2 uv = coords_to_uv(x, y, F.s);
+    int32_t dx, dy;
+    jittered_coords(F, uv, dx, dy);
+    f4 pd = load_position(F, A.G, dx, dy);
+    f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
+    float depth = pd.w;
+    Sample s = zero_sample();
+    Reservoir r = zero_reservoir();
+    if (F.indirect_bounces == 0u || depth < HK_F32_EPSILON) {
+        store_res(C.cur, idx, r);
+        store_res(C.spatial, idx, r);
+        store_res(C.prev_spatial, idx, r);
+        C.variance[idx] = 0.0f;
+        store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
+        return;
+    }
+    f3 normal = normalize(load_normal(F, A.G, dx, dy));
+    f2 imf = load_instance_material(F, A.G, dx, dy);
+    uint32_t im_x = f2u32(imf.x), im_y = f2u32(imf.y);
+    f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
+
+    s.random = noise_random(A.noise, F.number, x, y);
+    s.visible_position = mk4(position.x, position.y, position.z, depth);
+    s.visible_normal = normal;
+    s.visible_instance = im_x;
+
+    Ray ray;
+    HitInfo info;
+    float pdf = 0.0f;
+    Surface surface;
+
+    if (MULTI) {
+        Sample bs = s;
+        f3 ct = mk3(1.0f, 1.0f, 1.0f);
+        for (uint32_t n = 0u; n < F.indirect_bounces && (ct.x > 0.01f || ct.y > 0.01f || ct.z > 0.01f); n += 1u) {
+            f4 rs = sample_cosine_hemisphere(mk2(bs.random.x, bs.random.y));
+            ray.origin = xyz(bs.visible_position) + bs.visible_normal * RAY_BIAS;
+            f3 bt, bb;
+            normal_basis(bs.visible_normal, bt, bb);
+            ray.direction = basis_mul(bt, bb, bs.visible_normal, xyz(rs));
+            ray.inv_direction = inv(ray.direction);
+            n_top++;
+            Hit hit = traverse_top(A.sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+            info = hit_info(A.sc, ray, hit);
+            if (n == 0u) {
+                s.sample_position = info.position;
+                s.sample_normal = info.normal;
+                pdf = rs.w;
+            }
+            bs.sample_position = info.position;
+            bs.sample_normal = info.normal;
+            if (hit.instance_index != HK_U32_MAX) {
+                f3 out = mk3(0, 0, 0);
+                surface = retreive_surface(A.sc, info.material_index);
+                surface.roughness = 1.0f;
+                LightCandidate cand = select_light_candidate<true>(A.sc, F, bs.random, xyz(bs.sample_position),
+                                                                   bs.sample_normal, info.instance_index, info, n_emitter);
+                bool sample_directional = cand.emissive_instance == DONT_SAMPLE_EMISSIVE;
+                f3 bvd = normalize(xyz(bs.visible_position) - xyz(bs.sample_position));
+                if (dot(cand.direction, bs.sample_normal) > 0.0f && cand.p > 0.0f) {
+                    ray.origin = xyz(bs.sample_position) + bs.sample_normal * RAY_BIAS;
+                    ray.direction = cand.direction;
+                    ray.inv_direction = inv(ray.direction);
+                    n_top++;
+                    Hit sh = traverse_top(A.sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
+                    occlude_hit_info(ray, sh, info);
+                    f4 in_rad = input_radiance(A.sc, F, ray, info, sample_directional, cand.emissive_instance, false);
+                    out = shading(F, bvd, bs.sample_normal, ray.direction, surface, in_rad);
+                    out = out / cand.p;
+                    if (n > 0u) out = rs.w < 0.01f ? mk3(0, 0, 0) : out / rs.w;
+                    float ol = lum(out);
+                    if (ol > F.max_indirect_luminance) out = (out * F.max_indirect_luminance) / ol;
+                    f3 add = ct * out;
+                    s.radiance = mk4(s.radiance.x + add.x, s.radiance.y + add.y, s.radiance.z + add.z, s.radiance.w + 1.0f);
+                }
+                ct = ct * env_brdf(bvd, bs.sample_normal, surface);
+                float fn = (float)F.number * HK_GOLDEN_RATIO;
+                bs.random = mk4(hk_fract(bs.random.x + fn), hk_fract(bs.random.y + fn), hk_fract(bs.random.z + fn),
+                                hk_fract(bs.random.w + fn));
+                bs.visible_position = bs.sample_position;
+                bs.visible_normal = bs.sample_normal;
+            } else {
+                f3 out = xyz(input_radiance(A.sc, F, ray, info, false, DONT_SAMPLE_EMISSIVE, true));
+                f3 add = ct * out;
+                s.radiance = mk4(s.radiance.x + add.x, s.radiance.y + add.y, s.radiance.z + add.z, s.radiance.w + 0.0f);
+                break;
+            }
+        }
+    } else {
+        f4 rs = sample_cosine_hemisphere(mk2(s.random.x, s.random.y));
+        ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
+        f3 bt, bb;
+        normal_basis(s.visible_normal, bt, bb);
+        ray.direction = basis_mul(bt, bb, s.visible_normal, xyz(rs));
+        ray.inv_direction = inv(ray.direction);
+        n_top++;
+        Hit hit = traverse_top(A.sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+        info = hit_info(A.sc, ray, hit);
+        s.sample_position = info.position;
+        s.sample_normal = info.normal;
+        pdf = rs.w;
+        if (hit.instance_index != HK_U32_MAX) {
+            surface = retreive_surface(A.sc, info.material_index);
+            surface.roughness = 1.0f;
+            LightCandidate cand = select_light_candidate<true>(A.sc, F, s.random, xyz(s.sample_position), s.sample_normal,
+                                                               info.instance_index, info, n_emitter);
+            bool sample_directional = cand.emissive_instance == DONT_SAMPLE_EMISSIVE;
+            if (dot(cand.direction, s.sample_normal) > 0.0f && cand.p > 0.0f) {
+                ray.origin = xyz(s.sample_position) + s.sample_normal * RAY_BIAS;
+                ray.direction = cand.direction;
+                ray.inv_direction = inv(ray.direction);
+                n_top++;
+                Hit sh = traverse_top(A.sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
+                occlude_hit_info(ray, sh, info);
+                f4 in_rad = input_radiance(A.sc, F, ray, info, sample_directional, cand.emissive_instance, false);
+                f3 out = shading(F, normalize(xyz(s.visible_position) - xyz(s.sample_position)), s.sample_normal,
+                                 ray.direction, surface, in_rad);
+                out = out / cand.p;
+                s.radiance = mk4(s.radiance.x + out.x, s.radiance.y + out.y, s.radiance.z + out.z, s.radiance.w + 1.0f);
+            }
+        } else {
+            f3 out = xyz(input_radiance(A.sc, F, ray, info, false, DONT_SAMPLE_EMISSIVE, true));
+            s.radiance = mk4(s.radiance.x + out.x, s.radiance.y + out.y, s.radiance.z + out.z, s.radiance.w + 0.0f);
+        }
+    }
+
+    f2 juv = jittered_uv(F, uv, 0.25f);
+    f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
+    r = load_previous(F, C.prev, previous_uv);
+    if (!check_previous_reservoir(r, s) && uv_inside_closed(previous_uv)) {
+        int32_t px = f2i32(previous_uv.x * (float)F.s[0]);
+        int32_t py = f2i32(previous_uv.y * (float)F.s[1]);
+        store_res(C.prev_spatial, s_index(F, px, py), r);
+    }
+    surface = retreive_surface(A.sc, im_y);
+    f3 view_direction = calculate_view(F, position);
+    f3 sample_radiance = shading(F, view_direction, s.visible_normal,
+                                 normalize(xyz(s.sample_position) - xyz(s.visible_position)), surface, s.radiance);
+    float w_new = pdf > 0.0f ? lum(sample_radiance) / pdf : 0.0f;
+    temporal_restir(r, s, w_new, F.max_temporal_reuse_count);
+    f3 out = shading(F, view_direction, r.s.visible_normal, normalize(xyz(r.s.sample_position) - xyz(r.s.visible_position)),
+                     surface, r.s.radiance);
+    float total_lum = r.count * lum(out);
+    r.w = total_lum > 0.0f ? r.w_sum / total_lum : 0.0f;
+    r.s.visible_position = s.visible_position;
+    r.s.visible_normal = s.visible_normal;
+    r.lifetime += 1.0f;
+    C.variance[idx] = variance_of(r);
+    if (F.temporal_reuse > 0u) store_res(C.cur, idx, r);
+    f3 o = out * r.w;
+    store_rgba16f(C.render, idx, mk4(o.x, o.y, o.z, 1.0f));
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
+{
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, C, x, y, n_top, n_emitter);
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
+// ------------------------------------------------------------------ spatial_reuse (light.wgsl:1500-1684)
+// The reference's workgroup-shared copies (shared_reservoir/shared_depth) hold exactly the
+// values the global path reads for in-tile neighbours, so every neighbour is read from the
+// (L2-resident) reservoir planes directly.
+template <bool EMISSIVE_LIT>
+HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y)
+{
+    const Frame& F = A.F;
+    constexpr uint32_t COUNT = EMISSIVE_LIT ? 8u : 16u;
+    constexpr float RANGE = EMISSIVE_LIT ? 10.0f : 20.0f;
+    const int32_t idx = s_index(F, x, y);
+    const f2 uv = coords_to_uv(x, y, F.s);
+    int32_t dx, dy;
+    jittered_coords(F, uv, dx, dy);
+    f4 pd = load_position(F, A.G, dx, dy);
+    f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
+    float depth = pd.w;
+    Reservoir r = load_res(C.cur, idx);
+    if (depth < HK_F32_EPSILON) {
+        store_res(C.spatial, idx, r);
+        store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
+        return;
+    }
+    uint32_t im_y = f2u32(load_instance_material(F, A.G, dx, dy).y);
+    f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
+    Surface surface = retreive_surface(A.sc, im_y);
+    bool use_spatial_variance = r.count <= 4.0f;
+    f2 juv = jittered_uv(F, uv, 0.25f);
+    f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
+    Reservoir q = r;
+    const Sample s = q.s;
+    float lifetime_max = F.max_reservoir_lifetime <= 1.0f ? HK_F32_MAX : F.max_reservoir_lifetime;
+    if (r.lifetime <= lifetime_max) r = load_previous(F, C.prev_spatial, previous_uv);
+    f3 view_direction = calculate_view(F, position);
+    if (EMISSIVE_LIT) {
+        merge_reservoir(r, q, lum(xyz(q.s.radiance)));
+    } else {
+        f3 o = shading(F, view_direction, s.visible_normal, normalize(xyz(s.sample_position) - xyz(s.visible_position)),
+                       surface, s.radiance);
+        merge_reservoir(r, q, lum(o));
+    }
+    r.s.visible_position = s.visible_position;
+    r.s.visible_normal = s.visible_normal;
+
+    const float rf = hk_random_float(F.number);
+    const float srand = sum4(s.random);
+    for (uint32_t i = 1u; i <= COUNT; i += 1u) {
+        float px = HK_TAU * hk_fract(((float)i * HK_GOLDEN_RATIO + srand) + rf);
+        float py = sqrtf((float)i / (float)COUNT) * RANGE;
+        float sn, cs;
+        hk_sincos(px, &sn, &cs);
+        f2 offset = mk2(py * cs, py * sn);
+        int32_t scx = f2i32(offset.x + (float)x), scy = f2i32(offset.y + (float)y);
+        f2 suv = coords_to_uv(scx, scy, F.s);
+        if (suv.x < 0.0f || suv.y < 0.0f || suv.x > 1.0f || suv.y > 1.0f) continue;
+        int32_t sdx, sdy;
+        jittered_coords(F, suv, sdx, sdy);
+        float sample_depth = load_depth(F, A.G, sdx, sdy);
+        float depth_ratio = depth / sample_depth;
+        if (depth_ratio < 0.9f || depth_ratio > 1.1f) continue;
+        q = load_res(C.cur, s_index(F, scx, scy));
+        bool normal_miss = dot(s.visible_normal, q.s.visible_normal) < 0.866f;
+        if (q.count < HK_F32_EPSILON || normal_miss) continue;
+        f3 sample_direction = normalize(xyz(q.s.sample_position) - xyz(s.visible_position));
+        if (dot(sample_direction, s.visible_normal) < 0.0f) continue;
+
+        float tap_interval = fmaxf(1.0f, py / 5.0f);
+        uint32_t tap_count = f2u32(py / tap_interval);
+        bool occluded = false;
+        float inv_len = 1.0f / sqrtf(dot(offset, offset));
+        f2 dir = mk2(offset.x * inv_len, offset.y * inv_len);
+        for (uint32_t j = 1u; j <= tap_count; j += 1u) {
+            float tap_dist = (float)j * tap_interval;
+            f2 tuv = mk2(uv.x + (tap_dist * dir.x) / (float)F.s[0], uv.y + (tap_dist * dir.y) / (float)F.s[1]);
+            int32_t tdx, tdy;
+            jittered_coords(F, tuv, tdx, tdy);
+            float tap_depth = load_depth(F, A.G, tdx, tdy);
+            float ref_depth = hk_mixf(depth, sample_depth, (float)j / (float)(tap_count + 1u));
+            if (tap_depth > ref_depth + 0.00001f) {
+                occluded = true;
+                break;
+            }
+        }
+        if (occluded) continue;
+        float jacobian = q.s.sample_position.w > 0.5f ? compute_jacobian(q.s, s) : 1.0f;
+        if (EMISSIVE_LIT) {
+            merge_reservoir(r, q, lum(xyz(q.s.radiance)) / jacobian);
+        } else {
+            f3 o = shading(F, view_direction, s.visible_normal, sample_direction, surface, q.s.radiance);
+            merge_reservoir(r, q, lum(o) / jacobian);
+        }
+    }
+    float m = (float)F.max_spatial_reuse_count;
+    if (r.count > m) {
+        r.w_sum *= m / r.count;
+        r.w2_sum *= m / r.count;
+        r.count = m;
+    }
+    f3 out = shading(F, view_direction, s.visible_normal, normalize(xyz(r.s.sample_position) - xyz(s.visible_position)),
+                     surface, r.s.radiance);
+    float total_lum = EMISSIVE_LIT ? r.count * lum(xyz(r.s.radiance)) : r.count * lum(out);
+    r.w = total_lum > 0.0f ? r.w_sum / total_lum : 0.0f;
+    r.lifetime += 1.0f;
+    store_res(C.spatial, idx, r);
+    if (use_spatial_variance) C.variance[idx] = variance_of(r);
+    f3 oc = out * r.w;
+    store_rgba16f(C.render, idx, mk4(oc.x, oc.y, oc.z, 1.0f));
+}
+
+template <bool EMISSIVE_LIT>
+__global__ __launch_bounds__(256) void k_spatial(FrameArgs A, ChannelArgs C)
+{
+    int32_t x, y;
+    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y);
+}
+
+// ------------------------------------------------------------------ denoise (denoise.wgsl)
+__constant__ float KERNEL3[3][3] = {{0.0625f, 0.125f, 0.0625f}, {0.125f, 0.25f, 0.125f}, {0.0625f, 0.125f, 0.0625f}};
+
+HKD bool uv_outside(f2 uv) { return uv.x < 0.0f || uv.y < 0.0f || uv.x > 1.0f || uv.y > 1.0f; }
+HKD bool bad3(f3 v)
+{
+    return (v.x != v.x) || (v.y != v.y) || (v.z != v.z) || v.x > HK_F32_MAX || v.y > HK_F32_MAX || v.z > HK_F32_MAX;
+}
+// albedo plane is S-sized (band-local rows)
+HKD f4 load_albedo(const Frame& F, const uint2* albedo, int32_t x, int32_t y)
+{
+    return load_rgba16f(albedo, band_index(x, y, F.S[0], F.S_row0, F.S_rows));
+}
+
+__global__ __launch_bounds__(256) void k_demod(FrameArgs A, DenoiseArgs D)
+{
+    const Frame& F = A.F;
+    int32_t x, y;
+    if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    const int32_t idx = s_index(F, x, y);
+    f2 uv = coords_to_uv(x, y, F.s);
+    f2 duv = jittered_uv(F, uv, 0.5f);
+    int32_t ax, ay, rx, ry;
+    nearest_texel(duv, F.S, ax, ay);
+    f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
+    nearest_texel(uv, F.s, rx, ry);
+    f3 irr = xyz(load_rgba16f(D.render, s_index(F, rx, ry)));
+    irr = mk3(albedo.x < 0.01f ? 0.0f : irr.x / albedo.x, albedo.y < 0.01f ? 0.0f : irr.y / albedo.y,
+              albedo.z < 0.01f ? 0.0f : irr.z / albedo.z);
+    store_rgba16f(D.internal[0], idx, mk4(irr.x, irr.y, irr.z, 1.0f));
+    float sum_variance = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const int ox = k / 3 - 1, oy = k % 3 - 1;  // (-1,-1),(-1,0),(-1,1),(0,-1),...
+        f2 suv = mk2(uv.x + (float)ox / (float)F.s[0], uv.y + (float)oy / (float)F.s[1]);
+        if (uv_outside(suv)) continue;
+        int32_t vx, vy;
+        nearest_texel(suv, F.s, vx, vy);
+        float v = D.variance[s_index(F, vx, vy)];
+        if (v > HK_F32_MAX) continue;
+        sum_variance += KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
+    }
+    D.internal_variance[idx] = sum_variance;
+}
+
+template <bool FIREFLY>
+__global__ __launch_bounds__(256) void k_denoise(FrameArgs A, DenoiseArgs D, int level)
+{
+    const Frame& F = A.F;
+    int32_t x, y;
+    if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    const int32_t idx = s_index(F, x, y);
+    const uint2* input = D.internal[level];
+    uint2* output = level == 3 ? D.output : D.internal[level + 1];
+    const int32_t step = 8 >> level;
+    f2 uv = coords_to_uv(x, y, F.s);
+    f2 duv = jittered_uv(F, uv, 0.5f);
+    int32_t gx, gy;
+    nearest_texel(duv, F.S, gx, gy);
+    float depth = load_depth(F, A.G, gx, gy);
+    f2 depth_gradient = load_depth_gradient(F, A.G, gx, gy);
+    f3 normal = normalize(load_normal(F, A.G, gx, gy));
+    float instance = load_instance_material(F, A.G, gx, gy).x;
+    if (depth < HK_F32_EPSILON) {
+        store_rgba16f(output, idx, mk4(0, 0, 0, 0));
+        return;
+    }
+    float variance = D.internal_variance[idx];
+    f3 irradiance = xyz(load_rgba16f(input, idx));
+    f3 sum_irr = irradiance * 0.25f;
+    float sum_w = 0.25f;
+    if (bad3(irradiance)) {
+        irradiance = mk3(0, 0, 0);
+        sum_irr = mk3(0, 0, 0);
+        sum_w = 0.0f;
+    }
+    const float l0 = lum(irradiance);
+    const float lum_denom = 4.0f * hk_pow(variance, 0.25f) + 0.001f;
+    float m1 = 0.0f, m2 = 0.0f, cnt = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int kk = k < 4 ? k : k + 1;  // skip the centre
+        const int ox = kk % 3 - 1, oy = kk / 3 - 1;  // (-1,-1),(0,-1),(1,-1),(-1,0),(1,0),(-1,1),(0,1),(1,1)
+        int32_t sx = x + ox * step, sy = y + oy * step;
+        f2 suv = coords_to_uv(sx, sy, F.s);
+        if (uv_outside(suv)) continue;
+        f3 irr = xyz(load_rgba16f(input, s_index(F, sx, sy)));
+        if (bad3(irr)) continue;
+        f2 sduv = jittered_uv(F, suv, 0.5f);
+        int32_t tx, ty;
+        nearest_texel(sduv, F.S, tx, ty);
+        f3 sn = normalize(load_normal(F, A.G, tx, ty));
+        float sd = load_depth(F, A.G, tx, ty);
+        float si = load_instance_material(F, A.G, tx, ty).x;
+        float sl = lum(irr);
+        float w_normal = hk_pow(fmaxf(0.0f, dot(normal, sn)), 16.0f);
+        float w_depth = hk_exp((-fabsf(depth - sd)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
+        float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
+        float w_lum = hk_exp((-fabsf(l0 - sl)) / lum_denom);
+        float w = hk_clampf(((w_normal * w_depth) * w_instance) * w_lum, 0.0f, 1.0f) * KERNEL3[oy + 1][ox + 1];
+        sum_irr = sum_irr + irr * w;
+        sum_w += w;
+        if (FIREFLY) {
+            m1 += sl;
+            m2 += sl * sl;
+            cnt += 1.0f;
+        }
+    }
+    irradiance = sum_w < 0.0001f ? mk3(0, 0, 0) : sum_irr / sum_w;
+    if (FIREFLY) {
+        float mean = m1 / cnt;
+        float var = m2 / cnt - mean * mean;
+        if (l0 > mean + 3.0f * sqrtf(var)) irradiance = irradiance * (mean / l0);
+    }
+    f4 color = mk4(irradiance.x, irradiance.y, irradiance.z, 1.0f);
+    if (level == 3) {
+        f4 a = load_albedo(F, D.albedo, gx, gy);
+        color = mk4(color.x * a.x, color.y * a.y, color.z * a.z, color.w * a.w);
+    }
+    store_rgba16f(output, idx, color);
+}
+
+// ------------------------------------------------------------------ tone mapping (tone_mapping.wgsl:21-32)
+__global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
+{
+    const Frame& F = A.F;
+    int32_t x, y;
+    if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    const int32_t idx = s_index(F, x, y);
+    f4 c = load_rgba16f(T.direct, idx);
+    f4 e = load_rgba16f(T.emissive, idx);
+    c = mk4(c.x + e.x, c.y + e.y, c.z + e.z, c.w + e.w);
+    if (T.indirect) {
+        f4 i = load_rgba16f(T.indirect, idx);
+        c = mk4(c.x + i.x, c.y + i.y, c.z + i.z, c.w + i.w);
+    }
+    f3 cc = vmax(xyz(c), mk3(0.0039f, 0.0039f, 0.0039f));
+    float l_old = lum(cc);
+    float l_new = l_old / (1.0f + l_old);
+    cc = cc * (l_new / l_old);
+    f4 o = c.w > 0.0f ? mk4(cc.x, cc.y, cc.z, c.w) : mk4(F.clear_color[0], F.clear_color[1], F.clear_color[2], F.clear_color[3]);
+    store_rgba16f(T.output, idx, o);
+}
+
+// ------------------------------------------------------------------ stand-alone ray query
+__global__ __launch_bounds__(256) void k_trace(Scene sc, const float* rays, const float* max_d, const float* early_d,
+                                               const uint32_t* excl, uint32_t n, uint32_t* hits, unsigned long long* top)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t cnt = 0;
+    if (i < n) {
+        cnt = 1;
+        Ray ray;
+        ray.origin = ld3(rays + 6 * (size_t)i);
+        ray.direction = ld3(rays + 6 * (size_t)i + 3);
+        ray.inv_direction = inv(ray.direction);
+        Hit h = traverse_top(sc, ray, max_d ? max_d[i] : HK_F32_MAX, early_d ? early_d[i] : 0.0f,
+                             excl ? excl[i] : DONT_EXCLUDE);
+        uint32_t* o = hits + 5 * (size_t)i;
+        o[0] = __float_as_uint(h.uv.x);
+        o[1] = __float_as_uint(h.uv.y);
+        o[2] = __float_as_uint(h.distance);
+        o[3] = h.instance_index;
+        o[4] = h.primitive_index;
+    }
+    wave_count(top, cnt);
+}
+
+// ------------------------------------------------------------------ launchers
+static dim3 tiles(uint32_t width, int32_t rows) { return dim3((width + 15u) / 16u, ((uint32_t)rows + 15u) / 16u, 1); }
+
+void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_gbuffer, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, V);
+}
+void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_albedo, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, albedo);
+}
+void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
+{
+    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    if (emissive_lit) hipLaunchKernelGGL((k_direct<true, false>), g, dim3(256), 0, st, A, C);
+    else hipLaunchKernelGGL((k_direct<false, true>), g, dim3(256), 0, st, A, C);
+}
+void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st)
+{
+    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    if (multi) hipLaunchKernelGGL(k_indirect<true>, g, dim3(256), 0, st, A, C);
+    else hipLaunchKernelGGL(k_indirect<false>, g, dim3(256), 0, st, A, C);
+}
+void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
+{
+    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    if (emissive_lit) hipLaunchKernelGGL(k_spatial<true>, g, dim3(256), 0, st, A, C);
+    else hipLaunchKernelGGL(k_spatial<false>, g, dim3(256), 0, st, A, C);
+}
+void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_demod, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, D);
+}
+void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, bool firefly, hipStream_t st)
+{
+    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    if (firefly) hipLaunchKernelGGL(k_denoise<true>, g, dim3(256), 0, st, A, D, level);
+    else hipLaunchKernelGGL(k_denoise<false>, g, dim3(256), 0, st, A, D, level);
+}
+void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_tone, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
+}
+void launch_trace(const Scene& sc, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl,
+                  uint32_t n, uint32_t* hits, unsigned long long* top, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_trace, dim3((n + 255u) / 256u), dim3(256), 0, st, sc, rays, max_d, early_d, excl, n, hits, top);
+}
+
+}  // namespace hk

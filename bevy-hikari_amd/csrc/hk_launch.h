@@ -1,0 +1,63 @@
+// hk_launch.h — kernel argument blocks and launchers shared by hk_kernels.hip and the
+// host runtime (hk_runtime.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hk_device.h"
+
+namespace hk {
+
+struct FrameArgs {
+    Scene sc;
+    Frame F;
+    GBuffer G;
+    const uchar4* noise;  // 16 x 64 x 64 RGBA8
+    Counters cnt;
+};
+
+// One channel's bindings: group 5 (variance/render) + group 6 (reservoir pair) of light.rs:455-555.
+struct ChannelArgs {
+    ResBuf prev;          // previous_reservoir_buffer  (read)
+    ResBuf cur;           // reservoir_buffer            (write)
+    ResBuf prev_spatial;  // previous_spatial_reservoir_buffer
+    ResBuf spatial;       // spatial_reservoir_buffer
+    float* variance;
+    uint2* render;
+};
+
+struct ViewArgs {
+    float world_position[3];
+    float view_proj[16];
+    float inverse_view_proj[16];
+};
+
+struct DenoiseArgs {
+    const uint2* albedo;   // S
+    const uint2* render;   // s
+    const float* variance; // s
+    uint2* internal[4];
+    float* internal_variance;
+    uint2* output;
+};
+
+struct ToneArgs {
+    const uint2* direct;
+    const uint2* emissive;
+    const uint2* indirect;  // may be null (indirect_bounces == 0)
+    uint2* output;
+};
+
+void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, hipStream_t st);
+void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st);
+void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);
+void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st);
+void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);
+void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st);
+void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, bool firefly, hipStream_t st);
+void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st);
+void launch_trace(const Scene& sc, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl,
+                  uint32_t n, uint32_t* hits, unsigned long long* top, hipStream_t st);
+
+}  // namespace hk

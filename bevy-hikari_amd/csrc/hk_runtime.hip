@@ -1,0 +1,744 @@
+// hk_runtime.hip — host runtime behind the C ABI (include/hikari_amd.h).
+//
+// One hk_ctx per camera entity owns everything the reference keeps per view:
+//   ReservoirCache (light.rs:342-363)        -> 10 SoA reservoir buffers in HBM
+//   LightTextures (light.rs:297-383)          -> albedo (S), variance[3], render[3] (s)
+//   PostProcessTextures denoise part (post_process.rs:710-714) -> internal[4], internal variance,
+//                                               denoised[3], tone-mapped output
+//   group-2 scene buffers (mesh_material/mod.rs:488-598) -> device copies of the std430 arrays
+// hk_render_frame issues the kernels in LightNode::run order (light.rs:646-699) and
+// hk_denoise in PostProcessNode::run order (post_process.rs:1190-1224).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hikari_amd.h"
+#include "hk_launch.h"
+
+using namespace hk;
+
+namespace {
+constexpr int32_t BAND_HALO = 40;  // >= 36 rows: 20 (spatial reuse) + 15 (a-trous) + 1 (variance blur)
+
+struct TimedLaunch {
+    const char* name;
+    hipEvent_t start, stop;
+};
+}  // namespace
+
+struct hk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string error;
+
+    // scene
+    void* buf[9] = {};
+    uint32_t count[9] = {};
+    bool has_scene = false;
+    uchar4* noise = nullptr;
+    bool has_noise = false;
+
+    // sizes
+    uint32_t S[2] = {0, 0}, s[2] = {0, 0};
+    float ratio = 1.0f;
+    int32_t S_row0 = 0, S_rows = 0, s_row0 = 0, s_rows = 0;
+    int32_t core_row0 = 0, core_rows = 0;
+    bool sized = false;
+
+    // G-buffer (band-local, S-wide)
+    float4* g_position = nullptr;
+    uint32_t* g_normal = nullptr;
+    float2* g_depth_gradient = nullptr;
+    float2* g_instance_material = nullptr;
+    float4* g_velocity_uv = nullptr;
+    // light targets
+    uint2* albedo = nullptr;
+    float* variance[3] = {};
+    uint2* render[3] = {};
+    uint4* reservoirs[HK_RESERVOIR_BUFFERS] = {};
+    uint32_t res_n = 0;
+    // denoise
+    uint2* internal[4] = {};
+    float* internal_variance = nullptr;
+    uint2* denoised[3] = {};
+    uint2* tone = nullptr;
+    // counters (top, emitter, primary)
+    unsigned long long* counters = nullptr;
+
+    // timing
+    bool timing = false;
+    std::vector<TimedLaunch> pending;
+    std::vector<hipEvent_t> event_pool;
+    std::vector<std::string> timing_names;
+    std::vector<double> timing_ms;
+    std::vector<uint64_t> timing_n;
+};
+
+namespace {
+
+int fail(hk_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->error = msg;
+    return code;
+}
+
+#define HK_HIP(c, expr)                                                                          \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return fail((c), HK_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+hipStream_t pick(hk_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+template <typename T>
+void release(T*& p)
+{
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+void free_targets(hk_ctx* c)
+{
+    release(c->g_position);
+    release(c->g_normal);
+    release(c->g_depth_gradient);
+    release(c->g_instance_material);
+    release(c->g_velocity_uv);
+    release(c->albedo);
+    for (int i = 0; i < 3; ++i) {
+        release(c->variance[i]);
+        release(c->render[i]);
+        release(c->denoised[i]);
+    }
+    for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) release(c->reservoirs[i]);
+    for (int i = 0; i < 4; ++i) release(c->internal[i]);
+    release(c->internal_variance);
+    release(c->tone);
+    c->sized = false;
+}
+
+hipEvent_t take_event(hk_ctx* c)
+{
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+// Launch wrapper: records HIP events around the kernel on its own stream when timing is on.
+template <typename F>
+void timed(hk_ctx* c, const char* name, hipStream_t st, F&& launch)
+{
+    if (!c->timing) {
+        launch();
+        return;
+    }
+    TimedLaunch t{name, take_event(c), take_event(c)};
+    (void)hipEventRecord(t.start, st);
+    launch();
+    (void)hipEventRecord(t.stop, st);
+    c->pending.push_back(t);
+}
+
+void flush_timing(hk_ctx* c)
+{
+    for (TimedLaunch& t : c->pending) {
+        (void)hipEventSynchronize(t.stop);
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, t.start, t.stop);
+        size_t k = 0;
+        for (; k < c->timing_names.size(); ++k)
+            if (c->timing_names[k] == t.name) break;
+        if (k == c->timing_names.size()) {
+            c->timing_names.push_back(t.name);
+            c->timing_ms.push_back(0.0);
+            c->timing_n.push_back(0);
+        }
+        c->timing_ms[k] += ms;
+        c->timing_n[k] += 1;
+        c->event_pool.push_back(t.start);
+        c->event_pool.push_back(t.stop);
+    }
+    c->pending.clear();
+}
+
+FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
+{
+    FrameArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.sc.vertices = (const hk_vertex*)c->buf[0];
+    A.sc.primitives = (const hk_primitive*)c->buf[1];
+    A.sc.asset_nodes = (const hk_node*)c->buf[2];
+    A.sc.alias_table = (const hk_alias_entry*)c->buf[3];
+    A.sc.instances = (const hk_instance*)c->buf[4];
+    A.sc.instance_nodes = (const hk_node*)c->buf[5];
+    A.sc.materials = (const hk_material*)c->buf[6];
+    A.sc.emissive_nodes = (const hk_node*)c->buf[7];
+    A.sc.emissives = (const hk_emissive*)c->buf[8];
+    A.sc.n_instances = c->count[4];
+    A.sc.n_instance_nodes = c->count[5];
+    A.sc.n_materials = c->count[6];
+    A.sc.n_emissive_nodes = c->count[7];
+    Frame& F = A.F;
+    hk_settings def;
+    hk_settings_default(&def);
+    if (!st) st = &def;
+    F.number = in ? in->frame_number : 0u;
+    F.direct_validate_interval = st->direct_validate_interval;
+    F.emissive_validate_interval = st->emissive_validate_interval;
+    F.max_temporal_reuse_count = st->max_temporal_reuse_count;
+    F.max_spatial_reuse_count = st->max_spatial_reuse_count;
+    F.indirect_bounces = st->indirect_bounces;
+    F.temporal_reuse = st->temporal_reuse;
+    F.max_reservoir_lifetime = st->max_reservoir_lifetime;
+    F.max_indirect_luminance = st->max_indirect_luminance;
+    F.upscale_ratio = c->ratio;
+    F.cos_solar_angle = hk_cos(st->solar_angle);  // same implementation as the device side
+    for (int i = 0; i < 4; ++i) F.clear_color[i] = st->clear_color[i];
+    if (in) {
+        for (int i = 0; i < 3; ++i) {
+            F.view_world_position[i] = in->view.world_position[i];
+            F.view_proj_z[i] = in->view.view_proj[4 * i + 2];
+            F.directional_color[i] = in->lights.directional_color[i];
+            F.direction_to_light[i] = in->lights.direction_to_light[i];
+            F.ambient_color[i] = in->lights.ambient_color[i];
+        }
+        F.orthographic = in->view.projection[15] == 1.0f;
+    }
+    F.S[0] = c->S[0];
+    F.S[1] = c->S[1];
+    F.s[0] = c->s[0];
+    F.s[1] = c->s[1];
+    F.S_row0 = c->S_row0;
+    F.S_rows = c->S_rows;
+    F.s_row0 = c->s_row0;
+    F.s_rows = c->s_rows;
+    A.G.position = c->g_position;
+    A.G.normal = c->g_normal;
+    A.G.depth_gradient = c->g_depth_gradient;
+    A.G.instance_material = c->g_instance_material;
+    A.G.velocity_uv = c->g_velocity_uv;
+    A.noise = c->noise;
+    A.cnt.top = c->counters;
+    A.cnt.emitter = c->counters + 1;
+    A.cnt.primary = c->counters + 2;
+    return A;
+}
+
+int check_ready(hk_ctx* c, bool need_scene)
+{
+    if (!c) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    if (need_scene && !c->has_scene) return fail(c, HK_ERR_STATE, "no scene uploaded (hk_scene_upload)");
+    if (need_scene && !c->has_noise) return fail(c, HK_ERR_STATE, "no blue noise uploaded (hk_set_noise)");
+    return HK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hk_abi_version(void) { return HK_ABI_VERSION; }
+
+void hk_settings_default(hk_settings* o)
+{
+    // HikariSettings::default() (lib.rs:435-455); upscale ratio defaults to SMAA_TU_2_0
+    o->direct_validate_interval = 3;
+    o->emissive_validate_interval = 5;
+    o->max_temporal_reuse_count = 50;
+    o->max_spatial_reuse_count = 800;
+    o->max_reservoir_lifetime = 100.0f;
+    o->solar_angle = 0.046f;
+    o->indirect_bounces = 1;
+    o->max_indirect_luminance = 10.0f;
+    // Color::rgb(0.4, 0.4, 0.4) is sRGB; as linear RGBA
+    float l = std::pow((0.4f + 0.055f) / 1.055f, 2.4f);
+    o->clear_color[0] = o->clear_color[1] = o->clear_color[2] = l;
+    o->clear_color[3] = 1.0f;
+    o->temporal_reuse = 1;
+    o->emissive_spatial_reuse = 0;
+    o->indirect_spatial_reuse = 1;
+    o->denoise = 1;
+    o->taa = 0;
+    o->upscale_ratio = 2.0f;
+}
+
+int hk_create(int device, hk_ctx** out)
+{
+    if (!out) return HK_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return HK_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return HK_ERR_INVALID;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HK_ERR_HIP;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HK_ERR_NO_DEVICE;
+    hk_ctx* c = new hk_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return HK_ERR_HIP;
+    }
+    *out = c;
+    return HK_OK;
+}
+
+void hk_destroy(hk_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_targets(c);
+    for (int i = 0; i < 9; ++i) release(c->buf[i]);
+    release(c->noise);
+    release(c->counters);
+    for (auto& t : c->pending) {
+        c->event_pool.push_back(t.start);
+        c->event_pool.push_back(t.stop);
+    }
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* hk_last_error(const hk_ctx* c) { return c ? c->error.c_str() : "null context"; }
+
+int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
+{
+    if (!c || !d) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    const hk_array* arr[9] = {&d->vertices, &d->primitives, &d->asset_nodes, &d->alias_table, &d->instances,
+                              &d->instance_nodes, &d->materials, &d->emissive_nodes, &d->emissives};
+    const size_t elem[9] = {sizeof(hk_vertex), sizeof(hk_primitive), sizeof(hk_node), sizeof(hk_alias_entry),
+                            sizeof(hk_instance), sizeof(hk_node), sizeof(hk_material), sizeof(hk_node),
+                            sizeof(hk_emissive)};
+    if (d->instances.count == 0 || d->materials.count == 0)
+        return fail(c, HK_ERR_INVALID, "scene needs at least one instance and one material");
+    for (int i = 0; i < 9; ++i)
+        if (arr[i]->count && !arr[i]->data) return fail(c, HK_ERR_INVALID, "scene array with count but no data");
+    HK_HIP(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 9; ++i) {
+        release(c->buf[i]);
+        size_t bytes = (size_t)(arr[i]->count ? arr[i]->count : 1) * elem[i];
+        HK_HIP(c, hipMalloc(&c->buf[i], bytes));
+        HK_HIP(c, hipMemset(c->buf[i], 0, bytes));
+        if (arr[i]->count) HK_HIP(c, hipMemcpy(c->buf[i], arr[i]->data, arr[i]->count * elem[i], hipMemcpyHostToDevice));
+        c->count[i] = arr[i]->count;
+    }
+    c->has_scene = true;
+    return HK_OK;
+}
+
+int hk_set_noise(hk_ctx* c, const uint8_t* rgba, uint32_t count, uint32_t size)
+{
+    if (!c || !rgba) return HK_ERR_INVALID;
+    if (count != 16 || size != 64) return fail(c, HK_ERR_INVALID, "blue noise must be 16 textures of 64x64 RGBA8");
+    (void)hipSetDevice(c->device);
+    if (!c->noise) HK_HIP(c, hipMalloc(&c->noise, 16 * 64 * 64 * 4));
+    HK_HIP(c, hipMemcpy(c->noise, rgba, 16 * 64 * 64 * 4, hipMemcpyHostToDevice));
+    c->has_noise = true;
+    return HK_OK;
+}
+
+int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows)
+{
+    if (!c || width == 0 || height == 0) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    ratio = ratio < 1.0f ? 1.0f : (ratio > 2.0f ? 2.0f : ratio);  // Upscale::ratio (lib.rs:501-505)
+    if (band_rows == 0) {
+        band_y0 = 0;
+        band_rows = height;
+    }
+    if (band_y0 + band_rows > height) return fail(c, HK_ERR_INVALID, "band outside the frame");
+    bool whole = band_y0 == 0 && band_rows == height;
+    if (!whole && ratio != 1.0f) return fail(c, HK_ERR_INVALID, "row bands require upscale ratio 1.0");
+    HK_HIP(c, hipStreamSynchronize(c->stream));
+    free_targets(c);
+    c->S[0] = width;
+    c->S[1] = height;
+    c->ratio = ratio;
+    float scale = 1.0f / ratio;  // light.rs:318-319: ceil(scale * size)
+    c->s[0] = (uint32_t)std::ceil(scale * (float)width);
+    c->s[1] = (uint32_t)std::ceil(scale * (float)height);
+    if (whole) {
+        c->S_row0 = 0;
+        c->S_rows = (int32_t)height;
+        c->s_row0 = 0;
+        c->s_rows = (int32_t)c->s[1];
+        c->core_row0 = 0;
+        c->core_rows = (int32_t)c->s[1];
+    } else {
+        int32_t r0 = (int32_t)band_y0 - BAND_HALO;
+        int32_t r1 = (int32_t)(band_y0 + band_rows) + BAND_HALO;
+        r0 = r0 < 0 ? 0 : r0;
+        r1 = r1 > (int32_t)height ? (int32_t)height : r1;
+        c->S_row0 = c->s_row0 = r0;
+        c->S_rows = c->s_rows = r1 - r0;
+        c->core_row0 = (int32_t)band_y0 - r0;
+        c->core_rows = (int32_t)band_rows;
+    }
+    size_t SP = (size_t)width * c->S_rows, sp = (size_t)c->s[0] * c->s_rows;
+    HK_HIP(c, hipMalloc(&c->g_position, SP * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->g_normal, SP * sizeof(uint32_t)));
+    HK_HIP(c, hipMalloc(&c->g_depth_gradient, SP * sizeof(float2)));
+    HK_HIP(c, hipMalloc(&c->g_instance_material, SP * sizeof(float2)));
+    HK_HIP(c, hipMalloc(&c->g_velocity_uv, SP * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->albedo, SP * sizeof(uint2)));
+    HK_HIP(c, hipMemset(c->g_position, 0, SP * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->g_normal, 0, SP * sizeof(uint32_t)));
+    HK_HIP(c, hipMemset(c->g_depth_gradient, 0, SP * sizeof(float2)));
+    HK_HIP(c, hipMemset(c->g_instance_material, 0, SP * sizeof(float2)));
+    HK_HIP(c, hipMemset(c->g_velocity_uv, 0, SP * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->albedo, 0, SP * sizeof(uint2)));
+    for (int i = 0; i < 3; ++i) {
+        HK_HIP(c, hipMalloc(&c->variance[i], sp * sizeof(float)));
+        HK_HIP(c, hipMalloc(&c->render[i], sp * sizeof(uint2)));
+        HK_HIP(c, hipMalloc(&c->denoised[i], sp * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->variance[i], 0, sp * sizeof(float)));
+        HK_HIP(c, hipMemset(c->render[i], 0, sp * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->denoised[i], 0, sp * sizeof(uint2)));
+    }
+    c->res_n = (uint32_t)sp;
+    for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) {
+        HK_HIP(c, hipMalloc(&c->reservoirs[i], 4 * sp * sizeof(uint4)));
+        HK_HIP(c, hipMemset(c->reservoirs[i], 0, 4 * sp * sizeof(uint4)));  // light.rs:355-358 zero-fill
+    }
+    for (int i = 0; i < 4; ++i) {
+        HK_HIP(c, hipMalloc(&c->internal[i], sp * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->internal[i], 0, sp * sizeof(uint2)));
+    }
+    HK_HIP(c, hipMalloc(&c->internal_variance, sp * sizeof(float)));
+    HK_HIP(c, hipMemset(c->internal_variance, 0, sp * sizeof(float)));
+    HK_HIP(c, hipMalloc(&c->tone, sp * sizeof(uint2)));
+    HK_HIP(c, hipMemset(c->tone, 0, sp * sizeof(uint2)));
+    HK_HIP(c, hipDeviceSynchronize());
+    c->sized = true;
+    return HK_OK;
+}
+
+int hk_band_info(const hk_ctx* c, int32_t* row0, int32_t* rows, int32_t* core_row0, int32_t* core_rows)
+{
+    if (!c || !c->sized) return HK_ERR_STATE;
+    if (row0) *row0 = c->s_row0;
+    if (rows) *rows = c->s_rows;
+    if (core_row0) *core_row0 = c->core_row0;
+    if (core_rows) *core_rows = c->core_rows;
+    return HK_OK;
+}
+
+int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
+{
+    int rc = check_ready(c, true);
+    if (rc) return rc;
+    if (!in) return fail(c, HK_ERR_INVALID, "null frame inputs");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    FrameArgs A = frame_args(c, nullptr, in);
+    ViewArgs V;
+    for (int i = 0; i < 3; ++i) V.world_position[i] = in->view.world_position[i];
+    std::memcpy(V.view_proj, in->view.view_proj, sizeof(V.view_proj));
+    std::memcpy(V.inverse_view_proj, in->view.inverse_view_proj, sizeof(V.inverse_view_proj));
+    timed(c, "gbuffer", st, [&] { launch_gbuffer(A, V, st); });
+    HK_HIP(c, hipGetLastError());
+    return HK_OK;
+}
+
+int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, int device_ptr, void* stream)
+{
+    if (!c || !data) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    size_t SP = (size_t)c->S[0] * c->S_rows;
+    void* dst = nullptr;
+    size_t need = 0;
+    switch (plane) {
+    case 0: dst = c->g_position; need = SP * 16; break;
+    case 1: dst = c->g_normal; need = SP * 4; break;
+    case 2: dst = c->g_depth_gradient; need = SP * 8; break;
+    case 3: dst = c->g_instance_material; need = SP * 8; break;
+    case 4: dst = c->g_velocity_uv; need = SP * 16; break;
+    default: return fail(c, HK_ERR_INVALID, "unknown G-buffer plane");
+    }
+    if (bytes != need) return fail(c, HK_ERR_INVALID, "G-buffer plane size mismatch");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    HK_HIP(c, hipMemcpyAsync(dst, data, bytes, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    if (!device_ptr) HK_HIP(c, hipStreamSynchronize(st));
+    return HK_OK;
+}
+
+static ChannelArgs channel(hk_ctx* c, uint32_t number, int ch)
+{
+    // LightBindGroup reservoir pairs (light.rs:518-546); head = frame % 2 (light.rs:376)
+    static const int pairs[3][2] = {{0, 4}, {2, 4}, {6, 8}};
+    uint32_t current = number % 2u, previous = 1u - current;
+    ChannelArgs C;
+    C.prev = ResBuf{c->reservoirs[current + pairs[ch][0]], c->res_n};
+    C.cur = ResBuf{c->reservoirs[previous + pairs[ch][0]], c->res_n};
+    C.prev_spatial = ResBuf{c->reservoirs[current + pairs[ch][1]], c->res_n};
+    C.spatial = ResBuf{c->reservoirs[previous + pairs[ch][1]], c->res_n};
+    C.variance = c->variance[ch];
+    C.render = c->render[ch];
+    return C;
+}
+
+int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in, void* stream)
+{
+    int rc = check_ready(c, true);
+    if (rc) return rc;
+    if (!settings || !in) return fail(c, HK_ERR_INVALID, "null settings or frame inputs");
+    float want = settings->upscale_ratio < 1.0f ? 1.0f : (settings->upscale_ratio > 2.0f ? 2.0f : settings->upscale_ratio);
+    if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    FrameArgs A = frame_args(c, settings, in);
+    timed(c, "full_screen_albedo", st, [&] { launch_albedo(A, c->albedo, st); });
+    ChannelArgs C0 = channel(c, A.F.number, 0);
+    timed(c, "direct_lit", st, [&] { launch_direct(A, C0, false, st); });
+    ChannelArgs C1 = channel(c, A.F.number, 1);
+    timed(c, "direct_emissive", st, [&] { launch_direct(A, C1, true, st); });
+    if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", st, [&] { launch_spatial(A, C1, true, st); });
+    ChannelArgs C2 = channel(c, A.F.number, 2);
+    bool multi = settings->indirect_bounces >= 2u;
+    timed(c, multi ? "indirect_multiple_bounces" : "indirect_lit_ambient", st, [&] { launch_indirect(A, C2, multi, st); });
+    if (settings->indirect_spatial_reuse) timed(c, "indirect_spatial_reuse", st, [&] { launch_spatial(A, C2, false, st); });
+    HK_HIP(c, hipGetLastError());
+    return HK_OK;
+}
+
+int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in, void* stream)
+{
+    int rc = check_ready(c, false);
+    if (rc) return rc;
+    if (!settings || !in) return fail(c, HK_ERR_INVALID, "null settings or frame inputs");
+    if (!settings->denoise) return HK_OK;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    FrameArgs A = frame_args(c, settings, in);
+    int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
+    for (int ch = 0; ch < channels; ++ch) {
+        DenoiseArgs D;
+        D.albedo = c->albedo;
+        D.render = c->render[ch];
+        D.variance = c->variance[ch];
+        for (int i = 0; i < 4; ++i) D.internal[i] = c->internal[i];
+        D.internal_variance = c->internal_variance;
+        D.output = c->denoised[ch];
+        timed(c, "demodulation", st, [&] { launch_demod(A, D, st); });
+        for (int level = 0; level < 4; ++level) {
+            bool ff = ch >= 1;  // denoise_direct has no FIREFLY_FILTERING (post_process.rs:1193-1197)
+            timed(c, ff ? "denoise_firefly" : "denoise", st, [&] { launch_denoise(A, D, level, ff, st); });
+        }
+    }
+    HK_HIP(c, hipGetLastError());
+    return HK_OK;
+}
+
+int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
+{
+    int rc = check_ready(c, false);
+    if (rc) return rc;
+    if (!settings) return fail(c, HK_ERR_INVALID, "null settings");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    hk_frame_inputs dummy;
+    std::memset(&dummy, 0, sizeof(dummy));
+    FrameArgs A = frame_args(c, settings, &dummy);
+    ToneArgs T;
+    T.direct = settings->denoise ? c->denoised[0] : c->render[0];
+    T.emissive = settings->denoise ? c->denoised[1] : c->render[1];
+    T.indirect = settings->indirect_bounces == 0u ? nullptr : (settings->denoise ? c->denoised[2] : c->render[2]);
+    T.output = c->tone;
+    timed(c, "tone_mapping", st, [&] { launch_tone(A, T, st); });
+    HK_HIP(c, hipGetLastError());
+    return HK_OK;
+}
+
+static void* output_ptr(hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* bpp)
+{
+    uint32_t W = c->s[0], H = (uint32_t)c->s_rows, B = 8;
+    void* p = nullptr;
+    switch (id) {
+    case HK_OUT_ALBEDO: p = c->albedo; W = c->S[0]; H = (uint32_t)c->S_rows; break;
+    case HK_OUT_VARIANCE_DIRECT: case HK_OUT_VARIANCE_EMISSIVE: case HK_OUT_VARIANCE_INDIRECT:
+        p = c->variance[id - HK_OUT_VARIANCE_DIRECT]; B = 4; break;
+    case HK_OUT_RENDER_DIRECT: case HK_OUT_RENDER_EMISSIVE: case HK_OUT_RENDER_INDIRECT:
+        p = c->render[id - HK_OUT_RENDER_DIRECT]; break;
+    case HK_OUT_DENOISED_DIRECT: case HK_OUT_DENOISED_EMISSIVE: case HK_OUT_DENOISED_INDIRECT:
+        p = c->denoised[id - HK_OUT_DENOISED_DIRECT]; break;
+    case HK_OUT_TONE_MAPPED: p = c->tone; break;
+    case HK_OUT_GBUF_POSITION: p = c->g_position; W = c->S[0]; H = (uint32_t)c->S_rows; B = 16; break;
+    case HK_OUT_GBUF_NORMAL: p = c->g_normal; W = c->S[0]; H = (uint32_t)c->S_rows; B = 4; break;
+    case HK_OUT_GBUF_DEPTH_GRADIENT: p = c->g_depth_gradient; W = c->S[0]; H = (uint32_t)c->S_rows; B = 8; break;
+    case HK_OUT_GBUF_INSTANCE_MATERIAL: p = c->g_instance_material; W = c->S[0]; H = (uint32_t)c->S_rows; B = 8; break;
+    case HK_OUT_GBUF_VELOCITY_UV: p = c->g_velocity_uv; W = c->S[0]; H = (uint32_t)c->S_rows; B = 16; break;
+    case HK_OUT_DENOISE_INTERNAL_VARIANCE: p = c->internal_variance; B = 4; break;
+    default: return nullptr;
+    }
+    if (w) *w = W;
+    if (h) *h = H;
+    if (bpp) *bpp = B;
+    return p;
+}
+
+int hk_output_info(const hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* bpp)
+{
+    if (!c || !c->sized) return HK_ERR_STATE;
+    return output_ptr(const_cast<hk_ctx*>(c), id, w, h, bpp) ? HK_OK : HK_ERR_INVALID;
+}
+
+const void* hk_output_device_ptr(hk_ctx* c, int id)
+{
+    if (!c || !c->sized) return nullptr;
+    return output_ptr(c, id, nullptr, nullptr, nullptr);
+}
+
+int hk_get_output(hk_ctx* c, int id, void* dst, size_t bytes, int to_host, void* stream)
+{
+    if (!c || !dst) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    uint32_t w, h, b;
+    void* p = output_ptr(c, id, &w, &h, &b);
+    if (!p) return fail(c, HK_ERR_INVALID, "unknown output id");
+    size_t need = (size_t)w * h * b;
+    if (bytes != need) return fail(c, HK_ERR_INVALID, "output size mismatch");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    HK_HIP(c, hipMemcpyAsync(dst, p, bytes, to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
+    if (to_host) HK_HIP(c, hipStreamSynchronize(st));
+    return HK_OK;
+}
+
+int hk_dump_reservoirs(hk_ctx* c, int id, hk_packed_reservoir* dst, size_t count, void* stream)
+{
+    if (!c || !dst || id < 0 || id >= HK_RESERVOIR_BUFFERS) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    if (count != c->res_n) return fail(c, HK_ERR_INVALID, "reservoir count mismatch");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    std::vector<uint4> planes((size_t)4 * c->res_n);
+    HK_HIP(c, hipMemcpyAsync(planes.data(), c->reservoirs[id], planes.size() * sizeof(uint4), hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    for (size_t i = 0; i < count; ++i) {
+        uint4* o = reinterpret_cast<uint4*>(dst + i);
+        for (int k = 0; k < 4; ++k) o[k] = planes[(size_t)k * c->res_n + i];
+    }
+    return HK_OK;
+}
+
+int hk_load_reservoirs(hk_ctx* c, int id, const hk_packed_reservoir* src, size_t count, void* stream)
+{
+    if (!c || !src || id < 0 || id >= HK_RESERVOIR_BUFFERS) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    if (count != c->res_n) return fail(c, HK_ERR_INVALID, "reservoir count mismatch");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    std::vector<uint4> planes((size_t)4 * c->res_n);
+    for (size_t i = 0; i < count; ++i) {
+        const uint4* s = reinterpret_cast<const uint4*>(src + i);
+        for (int k = 0; k < 4; ++k) planes[(size_t)k * c->res_n + i] = s[k];
+    }
+    HK_HIP(c, hipMemcpyAsync(c->reservoirs[id], planes.data(), planes.size() * sizeof(uint4), hipMemcpyHostToDevice, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    return HK_OK;
+}
+
+int hk_reset_counters(hk_ctx* c, void* stream)
+{
+    if (!c) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    HK_HIP(c, hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), pick(c, stream)));
+    return HK_OK;
+}
+
+int hk_read_counters(hk_ctx* c, hk_counters* out, void* stream)
+{
+    if (!c || !out) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    unsigned long long v[4];
+    HK_HIP(c, hipMemcpyAsync(v, c->counters, sizeof(v), hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    out->traverse_top = v[0];
+    out->traverse_emitter = v[1];
+    out->primary = v[2];
+    return HK_OK;
+}
+
+int hk_enable_kernel_timing(hk_ctx* c, int enable)
+{
+    if (!c) return HK_ERR_INVALID;
+    flush_timing(c);
+    c->timing = enable != 0;
+    c->timing_names.clear();
+    c->timing_ms.clear();
+    c->timing_n.clear();
+    return HK_OK;
+}
+
+int hk_kernel_timing(hk_ctx* c, const char** names, float* ms, int capacity)
+{
+    if (!c) return HK_ERR_INVALID;
+    flush_timing(c);
+    int n = (int)c->timing_names.size();
+    for (int i = 0; i < n && i < capacity; ++i) {
+        if (names) names[i] = c->timing_names[i].c_str();
+        if (ms) ms[i] = (float)(c->timing_ms[i] / (double)(c->timing_n[i] ? c->timing_n[i] : 1));
+    }
+    return n;
+}
+
+int hk_trace(hk_ctx* c, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl, uint32_t n,
+             void* hits, int device_ptrs, void* stream)
+{
+    if (!c || !rays || !hits) return HK_ERR_INVALID;
+    if (!c->has_scene) return fail(c, HK_ERR_STATE, "no scene uploaded (hk_scene_upload)");
+    if (n == 0) return HK_OK;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    FrameArgs A = frame_args(c, nullptr, nullptr);
+    if (device_ptrs) {
+        launch_trace(A.sc, rays, max_d, early_d, excl, n, (uint32_t*)hits, c->counters, st);
+        HK_HIP(c, hipGetLastError());
+        return HK_OK;
+    }
+    float *d_rays = nullptr, *d_max = nullptr, *d_early = nullptr;
+    uint32_t *d_excl = nullptr, *d_hits = nullptr;
+    HK_HIP(c, hipMalloc(&d_rays, (size_t)n * 24));
+    HK_HIP(c, hipMalloc(&d_hits, (size_t)n * 20));
+    HK_HIP(c, hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice));
+    if (max_d) {
+        HK_HIP(c, hipMalloc(&d_max, (size_t)n * 4));
+        HK_HIP(c, hipMemcpy(d_max, max_d, (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    if (early_d) {
+        HK_HIP(c, hipMalloc(&d_early, (size_t)n * 4));
+        HK_HIP(c, hipMemcpy(d_early, early_d, (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    if (excl) {
+        HK_HIP(c, hipMalloc(&d_excl, (size_t)n * 4));
+        HK_HIP(c, hipMemcpy(d_excl, excl, (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    launch_trace(A.sc, d_rays, d_max, d_early, d_excl, n, d_hits, c->counters, st);
+    HK_HIP(c, hipGetLastError());
+    HK_HIP(c, hipMemcpyAsync(hits, d_hits, (size_t)n * 20, hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    release(d_rays);
+    release(d_hits);
+    release(d_max);
+    release(d_early);
+    release(d_excl);
+    return HK_OK;
+}
+
+}  // extern "C"

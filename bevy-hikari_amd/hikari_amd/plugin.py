@@ -1,0 +1,174 @@
+"""`HikariPlugin` host mirror: one `HikariRenderer` per camera, driving libhikari_amd.so.
+
+The reference's per-frame render-graph work for a `hikari` camera is
+    PrepassNode::run (raster G-buffer)                 -> render_gbuffer()  (primary rays, f1)
+    LightNode::run (light.rs:590-702)                  -> render_frame()
+    PostProcessNode::run denoise block (post_process.rs:1190-1224) -> denoise()
+    tone_mapping dispatch (post_process.rs:1226-1234)  -> tone_sum()
+`HikariPlugin.frame()` runs them in that order, like the `hikari` sub-graph (lib.rs:238-367).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _abi
+from .scene import Scene, load_noise
+from .settings import HikariSettings, HikariUniversalSettings
+
+RESERVOIR_DTYPE = np.dtype([("radiance", "<u4", 2), ("random", "<u4", 2), ("visible_position", "<f4", 4),
+                            ("sample_position", "<f4", 4), ("visible_normal", "<u4"), ("sample_normal", "<u4"),
+                            ("reservoir", "<u4", 2)])
+assert RESERVOIR_DTYPE.itemsize == 64
+
+
+def _check(ctx, rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _abi.lib().hk_last_error(ctx).decode() if ctx else ""
+        raise _abi.HikariError(f"{what} failed ({rc}): {msg}")
+
+
+class HikariRenderer:
+    """A camera's integrator context (hk_ctx)."""
+
+    def __init__(self, device: int = 0):
+        L = _abi.lib()
+        h = C.c_void_p()
+        rc = L.hk_create(device, C.byref(h))
+        if rc != 0:
+            raise _abi.HikariError(f"hk_create({device}) failed ({rc}): no usable gfx950 device")
+        self._L = L
+        self.ctx = h.value
+        self.width = self.height = 0
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._L.hk_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- resources
+    def upload_scene(self, scene: Scene) -> None:
+        desc = scene.desc if scene.desc is not None else scene.build()
+        _check(self.ctx, self._L.hk_scene_upload(self.ctx, C.byref(desc)), "hk_scene_upload")
+
+    def set_noise(self, noise: Optional[np.ndarray] = None) -> None:
+        n = np.ascontiguousarray(load_noise() if noise is None else noise, np.uint8)
+        _check(self.ctx, self._L.hk_set_noise(self.ctx, n.ctypes.data, 16, 64), "hk_set_noise")
+
+    def resize(self, width: int, height: int, ratio: float = 1.0, band_y0: int = 0, band_rows: int = 0) -> None:
+        _check(self.ctx, self._L.hk_resize(self.ctx, width, height, ratio, band_y0, band_rows), "hk_resize")
+        self.width, self.height = width, height
+
+    def band_info(self):
+        v = [C.c_int32() for _ in range(4)]
+        _check(self.ctx, self._L.hk_band_info(self.ctx, *[C.byref(x) for x in v]), "hk_band_info")
+        return tuple(x.value for x in v)
+
+    # ---- per frame
+    def render_gbuffer(self, inputs: _abi.hk_frame_inputs, stream=None) -> None:
+        _check(self.ctx, self._L.hk_render_gbuffer(self.ctx, C.byref(inputs), stream), "hk_render_gbuffer")
+
+    def render_frame(self, settings: _abi.hk_settings, inputs: _abi.hk_frame_inputs, stream=None) -> None:
+        _check(self.ctx, self._L.hk_render_frame(self.ctx, C.byref(settings), C.byref(inputs), stream),
+               "hk_render_frame")
+
+    def denoise(self, settings: _abi.hk_settings, inputs: _abi.hk_frame_inputs, stream=None) -> None:
+        _check(self.ctx, self._L.hk_denoise(self.ctx, C.byref(settings), C.byref(inputs), stream), "hk_denoise")
+
+    def tone_sum(self, settings: _abi.hk_settings, stream=None) -> None:
+        _check(self.ctx, self._L.hk_tone_sum(self.ctx, C.byref(settings), stream), "hk_tone_sum")
+
+    # ---- readback
+    def output_info(self, output_id: int):
+        w, h, b = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check(self.ctx, self._L.hk_output_info(self.ctx, output_id, C.byref(w), C.byref(h), C.byref(b)),
+               "hk_output_info")
+        return w.value, h.value, b.value
+
+    def output(self, output_id: int) -> np.ndarray:
+        """Raw bytes of an output plane as (rows, width, bytes_per_pixel) uint8."""
+        w, h, b = self.output_info(output_id)
+        out = np.empty((h, w, b), np.uint8)
+        _check(self.ctx, self._L.hk_get_output(self.ctx, output_id, out.ctypes.data, out.nbytes, 1, None),
+               "hk_get_output")
+        return out
+
+    def output_device_ptr(self, output_id: int) -> int:
+        return self._L.hk_output_device_ptr(self.ctx, output_id)
+
+    def reservoirs(self, buffer_id: int) -> np.ndarray:
+        w, h, _ = self.output_info(_abi.OUT_VARIANCE[0])
+        out = np.empty(w * h, RESERVOIR_DTYPE)
+        _check(self.ctx, self._L.hk_dump_reservoirs(self.ctx, buffer_id, out.ctypes.data, w * h, None),
+               "hk_dump_reservoirs")
+        return out
+
+    def load_reservoirs(self, buffer_id: int, data: np.ndarray) -> None:
+        data = np.ascontiguousarray(data, RESERVOIR_DTYPE)
+        _check(self.ctx, self._L.hk_load_reservoirs(self.ctx, buffer_id, data.ctypes.data, len(data), None),
+               "hk_load_reservoirs")
+
+    def reset_counters(self) -> None:
+        _check(self.ctx, self._L.hk_reset_counters(self.ctx, None), "hk_reset_counters")
+
+    def counters(self) -> dict:
+        c = _abi.hk_counters()
+        _check(self.ctx, self._L.hk_read_counters(self.ctx, C.byref(c), None), "hk_read_counters")
+        return {"traverse_top": c.traverse_top, "traverse_emitter": c.traverse_emitter, "primary": c.primary}
+
+    def enable_kernel_timing(self, enable: bool = True) -> None:
+        _check(self.ctx, self._L.hk_enable_kernel_timing(self.ctx, int(enable)), "hk_enable_kernel_timing")
+
+    def kernel_timing(self) -> dict:
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        n = self._L.hk_kernel_timing(self.ctx, names, ms, 64)
+        return {names[i].decode(): float(ms[i]) for i in range(min(n, 64))}
+
+    def trace(self, rays: np.ndarray, max_distance=None, early_distance=None, exclude=None) -> np.ndarray:
+        """Stand-alone traverse_top over n rays (n, 6) -> (n, 5) uint32 {u, v, t bits, instance, primitive}."""
+        rays = np.ascontiguousarray(rays, np.float32)
+        n = len(rays)
+        hits = np.empty((n, 5), np.uint32)
+        keep = [None if a is None else np.ascontiguousarray(a, dt)
+                for a, dt in ((max_distance, np.float32), (early_distance, np.float32), (exclude, np.uint32))]
+        ptr = [None if a is None else a.ctypes.data for a in keep]
+        _check(self.ctx, self._L.hk_trace(self.ctx, rays.ctypes.data, ptr[0], ptr[1], ptr[2], n, hits.ctypes.data, 0,
+                                          None), "hk_trace")
+        return hits
+
+
+class HikariPlugin:
+    """`app.add_plugin(HikariPlugin)` for one camera: owns the renderer and the frame counter
+    (`FrameCounter`, view.rs:75-103; frame numbers 0, 1, 2, ...)."""
+
+    def __init__(self, scene: Scene, settings: HikariSettings = None, device: int = 0,
+                 universal: HikariUniversalSettings = None):
+        self.settings = settings or HikariSettings()
+        self.universal = universal or HikariUniversalSettings()
+        self.renderer = HikariRenderer(device)
+        self.renderer.set_noise()
+        if self.universal.build_mesh_acceleration_structure and self.universal.build_instance_acceleration_structure:
+            self.renderer.upload_scene(scene)
+        self.frame_number = 0
+
+    def resize(self, width: int, height: int, band_y0: int = 0, band_rows: int = 0):
+        self.renderer.resize(width, height, self.settings.upscale.ratio(), band_y0, band_rows)
+
+    def frame(self, camera, lights, gbuffer: bool = True, stream=None) -> None:
+        from .scene import frame_inputs
+        r = self.renderer
+        s = self.settings.to_c()
+        fi = frame_inputs(self.frame_number, camera, lights, r.width, r.height)
+        if gbuffer:
+            r.render_gbuffer(fi, stream)
+        r.render_frame(s, fi, stream)
+        if self.settings.denoise:
+            r.denoise(s, fi, stream)
+        r.tone_sum(s, stream)
+        self.frame_number += 1

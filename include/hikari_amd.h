@@ -1,0 +1,216 @@
+/*
+ * hikari_amd.h — C ABI of the MI355X-native bevy-hikari integrator (libhikari_amd.so).
+ *
+ * A Rust shim behind bevy-hikari's unchanged `HikariPlugin` / `HikariSettings` API binds
+ * these symbols.  Each entry point replaces one piece of the
+ * reference's render-world code:
+ *
+ *   hk_create / hk_destroy      one context per camera entity: owns what `ReservoirCache`
+ *                               (light.rs:342-363), `LightTextures` (light.rs:297-383) and the
+ *                               denoise part of `PostProcessTextures` (post_process.rs:622-747) own
+ *   hk_scene_upload             the group-2 storage buffers written by
+ *                               `MeshRenderAssets::set` (mesh.rs:43-58), `InstanceRenderAssets::set`
+ *                               (instance.rs:82-99) and `MaterialRenderAssets` (material.rs:196-202)
+ *   hk_set_noise                the 16 blue-noise textures of `NoiseTextures` (lib.rs:189-219)
+ *   hk_resize                   `prepare_light_textures` reallocation (light.rs:307-383), which
+ *                               zero-fills the 10 reservoir buffers (light.rs:353-360)
+ *   hk_set_gbuffer              group-1 deferred textures produced by `PrepassNode` (prepass.rs:769-851)
+ *   hk_render_gbuffer           primary-ray substitute for the raster prepass (prepass.wgsl:84-100)
+ *   hk_render_frame             `LightNode::run` (light.rs:590-702): albedo, then per channel the
+ *                               temporal pass and (if enabled) the spatial pass
+ *   hk_denoise                  the denoise block of `PostProcessNode::run` (post_process.rs:1190-1224)
+ *   hk_tone_sum                 the `tone_mapping` dispatch (post_process.rs:1226-1234)
+ *   hk_get_output               reading `LightTextures` / `denoise_render` / tone-mapping output
+ *   hk_trace                    stand-alone ray query over the TLAS/BLAS (light.wgsl:442-486)
+ *
+ * Conventions: every function returns 0 on success and a negative HK_ERR_* code on
+ * failure; `hk_last_error` returns the message.  No exceptions cross the ABI.  A context
+ * is externally synchronized (single-threaded, like one render-graph node).  `stream` is
+ * a hipStream_t (NULL = the context's own stream); all GPU work is enqueued on it and
+ * the functions return without waiting, except hk_get_output(..., to_host=1) and
+ * hk_read_counters.
+ */
+#ifndef HIKARI_AMD_H
+#define HIKARI_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "hk_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HK_ABI_VERSION 1
+
+enum {
+    HK_OK = 0,
+    HK_ERR_INVALID = -1,   /* bad argument / shape */
+    HK_ERR_HIP = -2,       /* HIP runtime failure */
+    HK_ERR_STATE = -3,     /* called in the wrong order (e.g. render before upload) */
+    HK_ERR_NO_DEVICE = -4, /* no gfx950 device */
+};
+
+typedef struct hk_ctx hk_ctx;
+
+/* A {pointer, element count} array in a scene upload. */
+typedef struct hk_array {
+    const void* data;
+    uint32_t count;
+} hk_array;
+
+/*
+ * Scene buffers in group-2 binding order (mesh_material_bindings.wgsl:5-22).  The node
+ * arrays carry their element count here (the WGSL `Nodes.count` header word).  The data is
+ * COPIED: the caller keeps ownership.  A new upload replaces the whole scene.
+ */
+typedef struct hk_scene_desc {
+    hk_array vertices;       /* hk_vertex,      binding 0 */
+    hk_array primitives;     /* hk_primitive,   binding 1 */
+    hk_array asset_nodes;    /* hk_node,        binding 2 */
+    hk_array alias_table;    /* hk_alias_entry, binding 3 */
+    hk_array instances;      /* hk_instance,    binding 4 */
+    hk_array instance_nodes; /* hk_node,        binding 5 */
+    hk_array materials;      /* hk_material,    binding 6 */
+    hk_array emissive_nodes; /* hk_node,        binding 7 */
+    hk_array emissives;      /* hk_emissive,    binding 8 */
+} hk_scene_desc;
+
+/*
+ * Field-for-field mirror of `HikariSettings` (lib.rs:400-433); defaults in
+ * hk_settings_default() follow lib.rs:435-455.
+ */
+typedef struct hk_settings {
+    uint32_t direct_validate_interval;
+    uint32_t emissive_validate_interval;
+    uint32_t max_temporal_reuse_count;
+    uint32_t max_spatial_reuse_count;
+    float max_reservoir_lifetime;
+    float solar_angle;
+    uint32_t indirect_bounces;
+    float max_indirect_luminance;
+    float clear_color[4]; /* linear RGBA */
+    uint32_t temporal_reuse;
+    uint32_t emissive_spatial_reuse;
+    uint32_t indirect_spatial_reuse;
+    uint32_t denoise;
+    uint32_t taa;           /* 0 = Jasmine, 1 = None (post-path, not run here) */
+    float upscale_ratio;    /* Upscale::ratio(), clamped to [1, 2] (lib.rs:501-505) */
+} hk_settings;
+
+/* The parts of Bevy's `View` uniform the integrator reads (light.wgsl:714-727). */
+typedef struct hk_view {
+    float world_position[3];
+    float _pad0;
+    float view_proj[16];         /* column-major */
+    float inverse_view_proj[16]; /* column-major, used by hk_render_gbuffer for ray generation */
+    float projection[16];        /* column-major; projection[3].w == 1 => orthographic */
+} hk_view;
+
+/* The parts of Bevy's `Lights` uniform the integrator reads (light.wgsl:611,832,847,855). */
+typedef struct hk_lights {
+    float directional_color[4];     /* lights.directional_lights[0].color */
+    float direction_to_light[3];    /* lights.directional_lights[0].direction_to_light */
+    float _pad0;
+    float ambient_color[4];         /* lights.ambient_color */
+} hk_lights;
+
+/* Per-frame inputs: FrameUniform.number (view.rs:141-192) + view + lights. */
+typedef struct hk_frame_inputs {
+    uint32_t frame_number;
+    uint32_t _pad[3];
+    hk_view view;
+    hk_lights lights;
+} hk_frame_inputs;
+
+/* Output planes readable with hk_get_output. Sizes are per pixel of the plane's extent. */
+typedef enum hk_output_id {
+    HK_OUT_ALBEDO = 0,            /* RGBA16F, S (physical size)      */
+    HK_OUT_VARIANCE_DIRECT = 1,   /* R32F, s                           */
+    HK_OUT_VARIANCE_EMISSIVE = 2,
+    HK_OUT_VARIANCE_INDIRECT = 3,
+    HK_OUT_RENDER_DIRECT = 4,     /* RGBA16F, s                        */
+    HK_OUT_RENDER_EMISSIVE = 5,
+    HK_OUT_RENDER_INDIRECT = 6,
+    HK_OUT_DENOISED_DIRECT = 7,   /* RGBA16F, s                        */
+    HK_OUT_DENOISED_EMISSIVE = 8,
+    HK_OUT_DENOISED_INDIRECT = 9,
+    HK_OUT_TONE_MAPPED = 10,      /* RGBA16F, s                        */
+    HK_OUT_GBUF_POSITION = 11,    /* float4, S */
+    HK_OUT_GBUF_NORMAL = 12,      /* uint32 snorm8x4, S */
+    HK_OUT_GBUF_DEPTH_GRADIENT = 13, /* float2, S */
+    HK_OUT_GBUF_INSTANCE_MATERIAL = 14, /* float2, S */
+    HK_OUT_GBUF_VELOCITY_UV = 15, /* float4, S */
+    HK_OUT_DENOISE_INTERNAL_VARIANCE = 16, /* R32F, s (last channel denoised) */
+    HK_OUT_COUNT = 17
+} hk_output_id;
+
+/* Reservoir buffer ids 0..9 as allocated by light.rs:350-361; the channel pairs
+ * (temporal, spatial) are (0,4), (2,4), (6,8) + frame parity (light.rs:518-546). */
+#define HK_RESERVOIR_BUFFERS 10
+
+/* Per-frame device counters (ray queries issued; Mrays/s numerator). */
+typedef struct hk_counters {
+    uint64_t traverse_top;      /* traverse_top calls (light.wgsl:442) */
+    uint64_t traverse_emitter;  /* emitter traverse_bottom calls in select_light_candidate (light.wgsl:687) */
+    uint64_t primary;           /* primary rays of hk_render_gbuffer */
+} hk_counters;
+
+/* ---- lifetime ---- */
+int hk_abi_version(void);
+int hk_create(int device, hk_ctx** out_ctx);
+void hk_destroy(hk_ctx* ctx);
+const char* hk_last_error(const hk_ctx* ctx);
+void hk_settings_default(hk_settings* out);
+
+/* ---- resources ---- */
+int hk_scene_upload(hk_ctx* ctx, const hk_scene_desc* scene);
+int hk_set_noise(hk_ctx* ctx, const uint8_t* rgba8, uint32_t count, uint32_t size);
+/* physical size S = (width, height); integrator size s = ceil(S / ratio) (light.rs:318-319).
+ * band_y0/band_rows select a horizontal band of the frame (multi-GPU); (0, height) = whole frame. */
+int hk_resize(hk_ctx* ctx, uint32_t width, uint32_t height, float upscale_ratio,
+              uint32_t band_y0, uint32_t band_rows);
+
+/* band geometry after hk_resize: local rows [0, rows) hold global rows [row0, row0+rows);
+ * the band's own (non-halo) rows are local [core_row0, core_row0+core_rows) */
+int hk_band_info(const hk_ctx* ctx, int32_t* row0, int32_t* rows, int32_t* core_row0, int32_t* core_rows);
+
+/* ---- per frame ---- */
+int hk_render_gbuffer(hk_ctx* ctx, const hk_frame_inputs* inputs, void* stream);
+/* plane: 0..4 = position, normal, depth_gradient, instance_material, velocity_uv
+ * (full S-sized planes, or the band's rows); device_ptr != 0 => data is a device pointer */
+int hk_set_gbuffer_plane(hk_ctx* ctx, int plane, const void* data, size_t bytes, int device_ptr,
+                         void* stream);
+int hk_render_frame(hk_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs,
+                    void* stream);
+int hk_denoise(hk_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs, void* stream);
+int hk_tone_sum(hk_ctx* ctx, const hk_settings* settings, void* stream);
+
+/* ---- readback / state ---- */
+int hk_output_info(const hk_ctx* ctx, int output_id, uint32_t* width, uint32_t* height,
+                   uint32_t* bytes_per_pixel);
+/* rows [row0, row0+rows) of the plane (rows = 0 => all) */
+int hk_get_output(hk_ctx* ctx, int output_id, void* dst, size_t bytes, int to_host, void* stream);
+const void* hk_output_device_ptr(hk_ctx* ctx, int output_id);
+/* copy reservoir buffer `id` (0..9) in the reference's AoS PackedReservoir layout */
+int hk_dump_reservoirs(hk_ctx* ctx, int id, hk_packed_reservoir* dst, size_t count, void* stream);
+int hk_load_reservoirs(hk_ctx* ctx, int id, const hk_packed_reservoir* src, size_t count, void* stream);
+int hk_reset_counters(hk_ctx* ctx, void* stream);
+int hk_read_counters(hk_ctx* ctx, hk_counters* out, void* stream);
+/* mean duration (ms) of each kernel of the last hk_render_frame/hk_denoise call, if timing is enabled */
+int hk_enable_kernel_timing(hk_ctx* ctx, int enable);
+int hk_kernel_timing(hk_ctx* ctx, const char** names, float* ms, int capacity);
+
+/* ---- stand-alone ray query (minimum slice: light.wgsl:442-486) ----
+ * rays: n records of {origin xyz, direction xyz} (6 floats, host or device memory)
+ * per ray: max_distance, early_distance, exclude_instance (arrays of n, may be NULL =>
+ * closest-hit defaults F32_MAX, 0, 0xFFFFFFFF).
+ * hits: n records of {u, v, distance (f32), instance_index, primitive_index (u32)}. */
+int hk_trace(hk_ctx* ctx, const float* rays, const float* max_distance, const float* early_distance,
+             const uint32_t* exclude_instance, uint32_t n, void* hits, int device_ptrs, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIKARI_AMD_H */

@@ -1,0 +1,232 @@
+/*
+ * hk_math.h — the pinned scalar math library used on BOTH sides of the parity check
+ * (the gcc-built CPU oracle and the hipcc-built gfx950 kernels).
+ *
+ * WGSL leaves sin/cos/exp/exp2/pow/log2 implementation-defined (a few ulp), so there is
+ * no single "reference" bit pattern for them.  To make CPU-vs-GPU parity bit-exact we
+ * fix ONE implementation of each built-in here, written only with IEEE-754 single
+ * operations that both targets round identically: +, -, *, correctly-rounded / and
+ * sqrt, rint/floor, integer bit manipulation.  Both sides compile with
+ * -ffp-contract=off, so no mul+add is ever fused.  Accuracy vs libm is checked by
+ * tests/test_math.py (<= 4 ulp on the ranges the integrator uses).
+ *
+ * Plain C99 + HIP: HK_HD marks functions callable from host and device.
+ */
+#ifndef HK_MATH_H
+#define HK_MATH_H
+
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define HK_HD __host__ __device__ static inline
+#else
+#define HK_HD static inline
+#endif
+
+#define HK_PI 3.141592653589793f
+#define HK_TAU 6.283185307f      /* light.wgsl:226 */
+#define HK_INV_TAU 0.159154943f  /* light.wgsl:227 */
+#define HK_F32_EPSILON 1.1920929E-7f
+#define HK_F32_MAX 3.402823466E+38f
+#define HK_GOLDEN_RATIO 1.618033989f
+
+typedef union { float f; uint32_t u; int32_t i; } hk_fbits;
+
+HK_HD uint32_t hk_f2u(float f) { hk_fbits b; b.f = f; return b.u; }
+HK_HD float hk_u2f(uint32_t u) { hk_fbits b; b.u = u; return b.f; }
+
+HK_HD float hk_minf(float a, float b) { return fminf(a, b); } /* IEEE minNum */
+HK_HD float hk_maxf(float a, float b) { return fmaxf(a, b); } /* IEEE maxNum */
+HK_HD float hk_clampf(float x, float lo, float hi) { return hk_minf(hk_maxf(x, lo), hi); }
+HK_HD float hk_saturate(float x) { return hk_clampf(x, 0.0f, 1.0f); }
+HK_HD float hk_fract(float x) { return x - floorf(x); }
+HK_HD float hk_absf(float x) { return hk_u2f(hk_f2u(x) & 0x7FFFFFFFu); }
+HK_HD float hk_signf(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+HK_HD float hk_mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+
+/* 2^x.  Range-reduce to n + f, |f| <= 0.5; degree-7 Taylor of e^(f ln2) in Horner form. */
+HK_HD float hk_exp2(float x)
+{
+    if (x != x) return x;
+    if (x >= 128.0f) return hk_u2f(0x7F800000u);
+    if (x < -151.0f) return 0.0f;
+    float n = rintf(x);
+    float f = x - n;
+    float p = 1.5252733804059840e-05f;        /* ln2^7/7! */
+    p = p * f + 1.5403530393381608e-04f;      /* ln2^6/6! */
+    p = p * f + 1.3333558146428443e-03f;      /* ln2^5/5! */
+    p = p * f + 9.6181291076284772e-03f;      /* ln2^4/4! */
+    p = p * f + 5.5504108664821580e-02f;      /* ln2^3/3! */
+    p = p * f + 2.4022650695910071e-01f;      /* ln2^2/2! */
+    p = p * f + 6.9314718055994531e-01f;      /* ln2 */
+    p = p * f + 1.0f;
+    int32_t ni = (int32_t)n;
+    if (ni >= -126) {
+        return p * hk_u2f((uint32_t)(ni + 127) << 23);
+    }
+    /* subnormal result: two exact-exponent steps, the last one rounds once */
+    return (p * hk_u2f((uint32_t)(ni + 64 + 127) << 23)) * hk_u2f((uint32_t)(-64 + 127) << 23);
+}
+
+HK_HD float hk_exp(float x) { return hk_exp2(x * 1.4426950408889634f); }
+
+/* log2(x): x = m * 2^e with m in [sqrt(1/2), sqrt(2)); log2(m) via atanh series of s=(m-1)/(m+1). */
+HK_HD float hk_log2(float x)
+{
+    if (x != x) return x;
+    if (x < 0.0f) return hk_u2f(0x7FC00000u);
+    if (x == 0.0f) return hk_u2f(0xFF800000u);
+    if (x == hk_u2f(0x7F800000u)) return x;
+    int32_t e = 0;
+    if (x < 1.17549435e-38f) { x = x * 8388608.0f; e = -23; } /* normalize subnormals */
+    uint32_t u = hk_f2u(x);
+    e += (int32_t)((u >> 23) & 0xFF) - 127;
+    float m = hk_u2f((u & 0x007FFFFFu) | 0x3F800000u); /* [1,2) */
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    float s = (m - 1.0f) / (m + 1.0f);
+    float s2 = s * s;
+    float p = 0.11111111111111111f;          /* 1/9 */
+    p = p * s2 + 0.14285714285714285f;       /* 1/7 */
+    p = p * s2 + 0.2f;                       /* 1/5 */
+    p = p * s2 + 0.33333333333333333f;       /* 1/3 */
+    p = p * s2 + 1.0f;
+    float lm = (p * s) * 2.8853900817779268f; /* 2/ln2 */
+    return (float)e + lm;
+}
+
+/* WGSL pow(x, y) = exp2(y * log2(x)) for x >= 0 (NaN for x < 0). */
+HK_HD float hk_pow(float x, float y) { return hk_exp2(y * hk_log2(x)); }
+
+/* sin/cos with Cody-Waite reduction by pi/2 and Taylor kernels on [-pi/4, pi/4]. */
+HK_HD float hk_sin_kernel(float r)
+{
+    float r2 = r * r;
+    float p = 2.7557319223985893e-06f;      /* 1/9! */
+    p = p * r2 - 1.9841269841269841e-04f;   /* 1/7! */
+    p = p * r2 + 8.3333333333333333e-03f;   /* 1/5! */
+    p = p * r2 - 1.6666666666666667e-01f;   /* 1/3! */
+    return r + (r * r2) * p;
+}
+
+HK_HD float hk_cos_kernel(float r)
+{
+    float r2 = r * r;
+    float p = 2.4801587301587302e-05f;      /* 1/8! */
+    p = p * r2 - 1.3888888888888889e-03f;   /* 1/6! */
+    p = p * r2 + 4.1666666666666667e-02f;   /* 1/4! */
+    p = p * r2 - 0.5f;
+    return 1.0f + r2 * p;
+}
+
+HK_HD void hk_sincos(float x, float* s, float* c)
+{
+    if (x != x || hk_absf(x) == hk_u2f(0x7F800000u)) {
+        *s = hk_u2f(0x7FC00000u);
+        *c = *s;
+        return;
+    }
+    float k = rintf(x * 0.63661977236758134f); /* 2/pi */
+    /* pi/2 split into three parts; the first two have short mantissas */
+    float r = x - k * 1.5703125f;
+    r = r - k * 4.837512969970703125e-4f;
+    r = r - k * 7.54978995489188216e-8f;
+    int32_t q = ((int32_t)k) & 3;
+    float sk = hk_sin_kernel(r);
+    float ck = hk_cos_kernel(r);
+    if (q == 0) { *s = sk; *c = ck; }
+    else if (q == 1) { *s = ck; *c = -sk; }
+    else if (q == 2) { *s = -sk; *c = -ck; }
+    else { *s = -ck; *c = sk; }
+}
+
+HK_HD float hk_sin(float x) { float s, c; hk_sincos(x, &s, &c); return s; }
+HK_HD float hk_cos(float x) { float s, c; hk_sincos(x, &s, &c); return c; }
+
+/* ---- texel packing (WGSL pack / unpack built-ins) ---- */
+
+/* f32 -> f16 bits, round-to-nearest-even, overflow -> inf, NaN -> quiet NaN. */
+HK_HD uint32_t hk_f32_to_f16(float f)
+{
+    uint32_t x = hk_f2u(f);
+    uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t ex = (x >> 23) & 0xFFu;
+    uint32_t man = x & 0x7FFFFFu;
+    if (ex == 0xFFu) return sign | 0x7C00u | (man ? 0x200u : 0u);
+    int32_t e = (int32_t)ex - 127 + 15;
+    if (e >= 31) return sign | 0x7C00u;
+    if (e <= 0) {
+        if (e < -10) return sign;
+        uint32_t m = man | 0x800000u;
+        uint32_t shift = (uint32_t)(14 - e);
+        uint32_t h = m >> shift;
+        uint32_t rem = m & ((1u << shift) - 1u);
+        uint32_t half = 1u << (shift - 1u);
+        if (rem > half || (rem == half && (h & 1u))) h++;
+        return sign | h;
+    }
+    uint32_t h = sign | ((uint32_t)e << 10) | (man >> 13);
+    uint32_t rem = man & 0x1FFFu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return h;
+}
+
+HK_HD float hk_f16_to_f32(uint32_t h)
+{
+    uint32_t sign = (h & 0x8000u) << 16;
+    uint32_t ex = (h >> 10) & 0x1Fu;
+    uint32_t man = h & 0x3FFu;
+    if (ex == 0) {
+        if (man == 0) return hk_u2f(sign);
+        /* subnormal: man * 2^-24, exact in f32 */
+        float v = (float)man * 5.9604644775390625e-08f;
+        return sign ? -v : v;
+    }
+    if (ex == 31) return hk_u2f(sign | 0x7F800000u | (man << 13));
+    return hk_u2f(sign | ((ex + 112u) << 23) | (man << 13));
+}
+
+HK_HD uint32_t hk_pack2x16float(float a, float b) { return hk_f32_to_f16(a) | (hk_f32_to_f16(b) << 16); }
+HK_HD float hk_unpack_lo16float(uint32_t v) { return hk_f16_to_f32(v & 0xFFFFu); }
+HK_HD float hk_unpack_hi16float(uint32_t v) { return hk_f16_to_f32(v >> 16); }
+
+/* pack2x16unorm: u16(round(clamp(e, 0, 1) * 65535)), round = nearest-even */
+HK_HD uint32_t hk_unorm16(float e) { return (uint32_t)rintf(hk_clampf(e, 0.0f, 1.0f) * 65535.0f); }
+HK_HD uint32_t hk_pack2x16unorm(float a, float b) { return hk_unorm16(a) | (hk_unorm16(b) << 16); }
+HK_HD float hk_unpack_unorm16(uint32_t v) { return (float)(v & 0xFFFFu) / 65535.0f; }
+
+/* pack4x8snorm: i8(round(clamp(e, -1, 1) * 127)) */
+HK_HD uint32_t hk_snorm8(float e) { return ((uint32_t)(int32_t)rintf(hk_clampf(e, -1.0f, 1.0f) * 127.0f)) & 0xFFu; }
+HK_HD uint32_t hk_pack4x8snorm(float x, float y, float z, float w)
+{
+    return hk_snorm8(x) | (hk_snorm8(y) << 8) | (hk_snorm8(z) << 16) | (hk_snorm8(w) << 24);
+}
+/* unpack4x8snorm component: max(f32(i8) / 127, -1) */
+HK_HD float hk_unpack_snorm8(uint32_t v, int c)
+{
+    int32_t i = (int32_t)(int8_t)((v >> (8 * c)) & 0xFFu);
+    return hk_maxf((float)i / 127.0f, -1.0f);
+}
+
+/* utils.wgsl:15-29 */
+HK_HD uint32_t hk_hash(uint32_t value)
+{
+    uint32_t state = value;
+    state = state ^ 2747636419u;
+    state = state * 2654435769u;
+    state = state ^ (state >> 16);
+    state = state * 2654435769u;
+    state = state ^ (state >> 16);
+    state = state * 2654435769u;
+    return state;
+}
+
+HK_HD float hk_random_float(uint32_t value) { return (float)hk_hash(value) / 4294967295.0f; }
+
+/* utils.wgsl:62-64 (Rec. 709) */
+HK_HD float hk_luminance(float r, float g, float b)
+{
+    return (r * 0.2126f + g * 0.7152f) + b * 0.0722f;
+}
+
+#endif /* HK_MATH_H */

@@ -1,0 +1,68 @@
+/*
+ * hk_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of bevy-hikari's per-pixel integrator and denoiser, used as the parity
+ * checker for the HIP product path (libhikari_amd.so).  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load liboracle.so; the product never links it.
+ *
+ * Parity status: the reference (WGSL under wgpu/Bevy 0.9.1) cannot be compiled or run in
+ * this environment (no rustc/cargo, no WGSL compiler, no Vulkan ICD) and ships
+ * no tests, golden vectors or fixtures.  The restatement is therefore pinned only by
+ * independent known-answer tests of its building blocks (tests/test_oracle_kat.py: numpy
+ * and pure-Python restatements of hash, f16/unorm/snorm packing, slab and triangle tests,
+ * traversal, reservoir update, denoise weights) — full-frame parity with the reference
+ * itself is UNPINNED.
+ *
+ * The oracle mirrors the WGSL structure: one function per entry point, stackless
+ * skip-pointer traversal, AoS PackedReservoir buffers, textures as row-major planes.
+ */
+#ifndef HK_ORACLE_H
+#define HK_ORACLE_H
+
+#include <stdint.h>
+#include "../include/hikari_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hko_ctx hko_ctx;
+
+/* scene: as for hk_scene_upload; noise: 16 x 64 x 64 RGBA8; S = (width, height) */
+hko_ctx* hko_create(const hk_scene_desc* scene, const uint8_t* noise, uint32_t width, uint32_t height,
+                    float upscale_ratio, int threads);
+void hko_destroy(hko_ctx* ctx);
+
+void hko_render_gbuffer(hko_ctx* ctx, const hk_frame_inputs* inputs);
+void hko_render_frame(hko_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs);
+void hko_denoise(hko_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs);
+void hko_tone_sum(hko_ctx* ctx, const hk_settings* settings);
+
+/* host pointer to an output plane (hk_output_id), NULL if unknown */
+void* hko_output(hko_ctx* ctx, int output_id, uint32_t* width, uint32_t* height, uint32_t* bpp);
+hk_packed_reservoir* hko_reservoirs(hko_ctx* ctx, int id, uint32_t* count);
+void hko_counters(hko_ctx* ctx, hk_counters* out);
+void hko_reset_counters(hko_ctx* ctx);
+
+/* light.wgsl:442-486 for n rays {origin, direction}; hits {u, v, t, instance, primitive} */
+void hko_trace(hko_ctx* ctx, const float* rays, const float* max_distance, const float* early_distance,
+               const uint32_t* exclude_instance, uint32_t n, void* hits);
+
+/* building blocks exposed for known-answer tests */
+float hko_intersects_aabb(const float* origin, const float* inv_dir, const float* mn, const float* mx);
+void hko_intersects_triangle(const float* origin, const float* dir, const float* v0, const float* v1,
+                             const float* v2, float* out_uvt);
+void hko_pack_reservoir_roundtrip(const float* fields, hk_packed_reservoir* packed, float* unpacked);
+float hko_pow(float x, float y);
+float hko_exp2(float x);
+float hko_log2(float x);
+float hko_sin(float x);
+float hko_cos(float x);
+uint32_t hko_f32_to_f16(float x);
+uint32_t hko_hash(uint32_t x);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,124 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (oracle/_build/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+The product (bevy-hikari_amd/hikari_amd) never does.  Parity status: see hk_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "liboracle.so"
+
+_L = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib() -> C.CDLL:
+    global _L
+    if _L is not None:
+        return _L
+    if not LIB.exists():
+        build()
+    L = C.CDLL(str(LIB))
+    vp, u32, f = C.c_void_p, C.c_uint32, C.c_float
+    sigs = {
+        "hko_create": (vp, [vp, vp, u32, u32, f, C.c_int]),
+        "hko_destroy": (None, [vp]),
+        "hko_render_gbuffer": (None, [vp, vp]),
+        "hko_render_frame": (None, [vp, vp, vp]),
+        "hko_denoise": (None, [vp, vp, vp]),
+        "hko_tone_sum": (None, [vp, vp]),
+        "hko_output": (vp, [vp, C.c_int, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]),
+        "hko_reservoirs": (vp, [vp, C.c_int, C.POINTER(u32)]),
+        "hko_counters": (None, [vp, vp]),
+        "hko_reset_counters": (None, [vp]),
+        "hko_trace": (None, [vp, vp, vp, vp, vp, u32, vp]),
+        "hko_intersects_aabb": (f, [vp, vp, vp, vp]),
+        "hko_intersects_triangle": (None, [vp, vp, vp, vp, vp, vp]),
+        "hko_pack_reservoir_roundtrip": (None, [vp, vp, vp]),
+        "hko_pow": (f, [f, f]),
+        "hko_exp2": (f, [f]),
+        "hko_log2": (f, [f]),
+        "hko_sin": (f, [f]),
+        "hko_cos": (f, [f]),
+        "hko_f32_to_f16": (u32, [f]),
+        "hko_hash": (u32, [u32]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _L = L
+    return L
+
+
+class Oracle:
+    """CPU restatement of one camera's integrator state (same API shape as HikariRenderer)."""
+
+    def __init__(self, scene_desc, noise: np.ndarray, width: int, height: int, ratio: float = 1.0, threads: int = 0):
+        L = lib()
+        self._L = L
+        self._noise = np.ascontiguousarray(noise, np.uint8)
+        self.ctx = L.hko_create(C.byref(scene_desc), self._noise.ctypes.data, width, height, ratio,
+                                threads or (os.cpu_count() or 1))
+        self.width, self.height = width, height
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._L.hko_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def render_gbuffer(self, inputs):
+        self._L.hko_render_gbuffer(self.ctx, C.byref(inputs))
+
+    def render_frame(self, settings, inputs):
+        self._L.hko_render_frame(self.ctx, C.byref(settings), C.byref(inputs))
+
+    def denoise(self, settings, inputs):
+        self._L.hko_denoise(self.ctx, C.byref(settings), C.byref(inputs))
+
+    def tone_sum(self, settings):
+        self._L.hko_tone_sum(self.ctx, C.byref(settings))
+
+    def output(self, output_id: int) -> np.ndarray:
+        w, h, b = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        p = self._L.hko_output(self.ctx, output_id, C.byref(w), C.byref(h), C.byref(b))
+        if not p:
+            raise KeyError(output_id)
+        n = w.value * h.value * b.value
+        return np.frombuffer(C.string_at(p, n), np.uint8).reshape(h.value, w.value, b.value).copy()
+
+    def reservoirs(self, buffer_id: int) -> np.ndarray:
+        from hikari_amd.plugin import RESERVOIR_DTYPE
+        cnt = C.c_uint32()
+        p = self._L.hko_reservoirs(self.ctx, buffer_id, C.byref(cnt))
+        return np.frombuffer(C.string_at(p, cnt.value * 64), RESERVOIR_DTYPE).copy()
+
+    def counters(self) -> dict:
+        v = (C.c_uint64 * 3)()
+        self._L.hko_counters(self.ctx, v)
+        return {"traverse_top": v[0], "traverse_emitter": v[1], "primary": v[2]}
+
+    def reset_counters(self):
+        self._L.hko_reset_counters(self.ctx)
+
+    def trace(self, rays, max_distance=None, early_distance=None, exclude=None) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, np.float32)
+        hits = np.empty((len(rays), 5), np.uint32)
+        keep = [None if a is None else np.ascontiguousarray(a, dt)
+                for a, dt in ((max_distance, np.float32), (early_distance, np.float32), (exclude, np.uint32))]
+        self._L.hko_trace(self.ctx, rays.ctypes.data, *[None if a is None else a.ctypes.data for a in keep],
+                          len(rays), hits.ctypes.data)
+        return hits
