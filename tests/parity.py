@@ -33,8 +33,8 @@ def canon_plane(output_id: int, raw: np.ndarray) -> np.ndarray:
 def canon_reservoirs(r: np.ndarray) -> np.ndarray:
     u = np.ascontiguousarray(r).view(np.uint32).reshape(-1, 16).copy()
     f16_words = [0, 1, 14, 15]  # radiance, reservoir (random is unorm16: compared raw)
-    halves = canon_f16(u[:, f16_words].view(np.uint16))
-    u[:, f16_words] = halves.view(np.uint32).reshape(u[:, f16_words].shape)
+    halves = canon_f16(np.ascontiguousarray(u[:, f16_words]).view(np.uint16))
+    u[:, f16_words] = halves.view(np.uint32).reshape(len(u), len(f16_words))
     u[:, 4:12] = canon_f32(u[:, 4:12])
     return u
 
