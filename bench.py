@@ -1,0 +1,251 @@
+"""Benchmark: bevy-hikari's headline path (per-pixel integrator [+ SVGF denoiser]) on MI355X.
+
+BASELINE.json metric: Mrays/sec + ms/frame @1080p 1spp.  Workload at N=1 = configs[1]:
+examples/cornell.rs at 1920x1080, 1 spp, traversal + NEE only (full-screen albedo, direct,
+emissive and indirect temporal passes; spatial reuse and denoise off).  One "step" = one
+frame: primary-ray G-buffer + hk_render_frame + tone-sum (+ denoise when enabled).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the frame is
+split into N row bands (plus a recomputed halo when spatial reuse/denoise read neighbours);
+each rank renders its band and the tone-mapped RGBA16F bands are all-gathered over RCCL, so
+every rank ends each step with the whole frame.  Total work is fixed => "strong" scaling.
+
+Mrays/s = traversal queries issued for the frame's own pixels (primary rays + every
+traverse_top + every emitter traverse_bottom of select_light_candidate; device counters,
+halo rows excluded) / wall time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "bevy-hikari_amd"))
+
+# torch first: libhikari_amd.so then binds to the HIP runtime torch already loaded (same soname,
+# libamdhip64.so.7), so device pointers, streams and RCCL share one runtime in this process.
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import hikari_amd  # noqa: E402
+from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# Compulsory HBM bytes per pixel per launch (reference texel formats; DESIGN.md "Roofline"):
+BYTES_PER_PIXEL = {
+    "gbuffer": 52,                   # writes position 16 + normal 4 + gradient 8 + ids 8 + velocity/uv 16
+    "full_screen_albedo": 52,        # reads 44 B of G-buffer, writes RGBA16F
+    "direct_lit": 184,               # G 44 + reservoir read 64 + write 64 + variance 4 + render 8
+    "direct_emissive": 184,
+    "indirect_lit_ambient": 184,
+    "indirect_multiple_bounces": 184,
+    "indirect_spatial_reuse": 244,   # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8
+    "emissive_spatial_reuse": 244,
+    "demodulation": 32,
+    "denoise": 56,
+    "denoise_firefly": 56,
+    "tone_mapping": 32,
+}
+
+CONFIGS = {
+    # BASELINE.json configs[1]
+    "cornell-1080p-nee": dict(scene="cornell", width=1920, height=1080, spatial=False, denoise=False,
+                              workload="examples/cornell.rs 1920x1080 1spp, traversal + NEE only "
+                                       "(albedo + direct + emissive + indirect temporal; denoise off)"),
+    # configs[2]
+    "scene-1080p-full": dict(scene="scene", width=1920, height=1080, spatial=True, denoise=True,
+                             workload="examples/scene.rs layout (City proxy geometry) 1920x1080 1spp + ReSTIR "
+                                      "temporal/spatial + SVGF denoise"),
+    # configs[3]
+    "city-4k": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True,
+                    workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, row bands + RCCL all-gather"),
+}
+
+
+def cpu_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))  # the GPU box grants 16 host cores to one GPU
+
+
+def cpu_baseline(scene_desc, cam, lights, st, w, h, budget_s: float) -> dict:
+    """The oracle (C restatement, OpenMP) on the same workload, bounded to ~budget_s seconds."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from oracle import Oracle  # test-infrastructure checker, used here only as the CPU baseline
+    threads = cpu_threads()
+    o = Oracle(scene_desc, hikari_amd.load_noise(), w, h, st.upscale.ratio(), threads=threads)
+    s = st.to_c()
+    rays = 0
+    frames = 0
+    t0 = time.perf_counter()
+    while frames < 64:
+        fi = frame_inputs(frames, cam, lights, w, h)
+        o.reset_counters()
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        if st.denoise:
+            o.denoise(s, fi)
+        o.tone_sum(s)
+        c = o.counters()
+        rays += c["traverse_top"] + c["traverse_emitter"] + c["primary"]
+        frames += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "ms_per_frame": round(dt / frames * 1e3, 1),
+            "sample": f"same workload, frames 0..{frames - 1} ({frames} frames, {dt:.1f} s) on the CPU oracle "
+                      f"(C restatement of light.wgsl/denoise.wgsl, {threads} OpenMP threads)"}
+
+
+def load_pmc_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), if present."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--config", default="cornell-1080p-nee", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    args = ap.parse_args()
+
+    cfg = CONFIGS[args.config]
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and world == 1 and args.gpus != 1:
+        print(f"warning: --gpus {args.gpus} without a distributed launcher; running 1 rank", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H = cfg["width"], cfg["height"]
+    scene, cam, lights = examples.SCENES[cfg["scene"]]()
+    desc = scene.build()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
+    s = st.to_c()
+
+    # row band of this rank
+    assert H % world == 0, "frame height must divide evenly into bands"
+    band = H // world
+    y0 = rank * band
+    r = HikariRenderer(local)
+    r.set_noise()
+    r.upload_scene(scene)
+    needs_halo = cfg["spatial"] or cfg["denoise"]
+    r.set_band_halo(40 if needs_halo else 0)
+    if world > 1:
+        r.resize(W, H, 1.0, y0, band)
+    else:
+        r.resize(W, H, 1.0)
+    row0, rows, core0, core_rows = r.band_info()
+
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    band_t = torch.empty((band, W, 4), dtype=torch.float16, device="cuda")
+    full_t = torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") if world > 1 else None
+
+    def step(f):
+        fi = frame_inputs(f, cam, lights, W, H)
+        r.render_gbuffer(fi, sp)
+        r.render_frame(s, fi, sp)
+        if st.denoise:
+            r.denoise(s, fi, sp)
+        r.tone_sum(s, sp)
+        if world > 1:
+            r.copy_output_rows(hikari_amd._abi.OUT_TONE_MAPPED, core0, core_rows, band_t.data_ptr(), False, sp)
+            dist.all_gather_into_tensor(full_t, band_t)
+
+    for f in range(args.warmup):
+        step(f)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    r.reset_counters()
+    r.enable_kernel_timing(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(args.warmup, args.warmup + args.steps):
+        step(f)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timing = r.kernel_timing()
+    c = r.counters()
+    rays = c["traverse_top"] + c["traverse_emitter"] + c["primary"]
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+        n = torch.tensor([rays], dtype=torch.float64, device="cuda")
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        rays = int(n.item())
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        mrays = rays / elapsed / 1e6
+        # roofline of the dominant kernel (largest total time per frame)
+        per_frame = {}
+        for name, avg in timing.items():
+            launches = {"denoise": 4, "denoise_firefly": 8, "demodulation": 3 if st.indirect_bounces else 2}.get(name, 1)
+            per_frame[name] = avg * launches
+        dom = max(per_frame, key=per_frame.get)
+        pix = W * rows
+        alg = BYTES_PER_PIXEL.get(dom, 0) * pix
+        achieved = alg / (timing[dom] * 1e-3) / 1e9
+        traffic = load_pmc_traffic(dom)
+        result = {
+            "metric": "Mrays/sec + ms/frame @1080p 1spp; cornell & city scenes, 1/2/4/8 GPU",
+            "value": round(mrays, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (static camera; reference assets: cornell.glb, blue noise)",
+            "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": 1,
+                       "rays_per_frame": int(rays // args.steps),
+                       "parallelism": f"row-bands x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": alg, "avg_ms": round(timing[dom], 4)},
+            "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
+        }
+        if world == 1 and args.cpu_budget > 0:
+            result["cpu_baseline"] = cpu_baseline(desc, cam, lights, st, W, H, args.cpu_budget)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result))
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -92,6 +92,7 @@ __global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V)
             A.G.velocity_uv[idx] = make_float4(0.0f, 0.0f, info.uv.x, info.uv.y);
         }
     }
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_primary = 0;
     wave_count(A.cnt.primary, n_primary);
 }
 
@@ -242,6 +243,7 @@ __global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_body<EMISSIVE_LIT, RENDER_EMISSIVE>(A, C, x, y, n_top, n_emitter);
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -411,6 +413,7 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, C, x, y, n_top, n_emitter);
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }

@@ -47,6 +47,7 @@ struct hk_ctx {
     float ratio = 1.0f;
     int32_t S_row0 = 0, S_rows = 0, s_row0 = 0, s_rows = 0;
     int32_t core_row0 = 0, core_rows = 0;
+    int32_t halo = BAND_HALO;
     bool sized = false;
 
     // G-buffer (band-local, S-wide)
@@ -222,6 +223,8 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     F.S_rows = c->S_rows;
     F.s_row0 = c->s_row0;
     F.s_rows = c->s_rows;
+    F.count_y0 = c->s_row0 + c->core_row0;
+    F.count_y1 = F.count_y0 + c->core_rows;
     A.G.position = c->g_position;
     A.G.normal = c->g_normal;
     A.G.depth_gradient = c->g_depth_gradient;
@@ -379,8 +382,8 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
         c->core_row0 = 0;
         c->core_rows = (int32_t)c->s[1];
     } else {
-        int32_t r0 = (int32_t)band_y0 - BAND_HALO;
-        int32_t r1 = (int32_t)(band_y0 + band_rows) + BAND_HALO;
+        int32_t r0 = (int32_t)band_y0 - c->halo;
+        int32_t r1 = (int32_t)(band_y0 + band_rows) + c->halo;
         r0 = r0 < 0 ? 0 : r0;
         r1 = r1 > (int32_t)height ? (int32_t)height : r1;
         c->S_row0 = c->s_row0 = r0;
@@ -424,6 +427,13 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
     HK_HIP(c, hipMemset(c->tone, 0, sp * sizeof(uint2)));
     HK_HIP(c, hipDeviceSynchronize());
     c->sized = true;
+    return HK_OK;
+}
+
+int hk_set_band_halo(hk_ctx* c, uint32_t rows)
+{
+    if (!c || rows > 4096) return HK_ERR_INVALID;
+    c->halo = (int32_t)rows;
     return HK_OK;
 }
 
@@ -615,6 +625,23 @@ int hk_get_output(hk_ctx* c, int id, void* dst, size_t bytes, int to_host, void*
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
     HK_HIP(c, hipMemcpyAsync(dst, p, bytes, to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
+    if (to_host) HK_HIP(c, hipStreamSynchronize(st));
+    return HK_OK;
+}
+
+int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* dst, int to_host, void* stream)
+{
+    if (!c || !dst) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    uint32_t w, h, b;
+    void* p = output_ptr(c, id, &w, &h, &b);
+    if (!p) return fail(c, HK_ERR_INVALID, "unknown output id");
+    if (row0 + rows > h) return fail(c, HK_ERR_INVALID, "row range outside the plane");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    size_t pitch = (size_t)w * b;
+    HK_HIP(c, hipMemcpyAsync(dst, (const char*)p + (size_t)row0 * pitch, (size_t)rows * pitch,
+                             to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
     if (to_host) HK_HIP(c, hipStreamSynchronize(st));
     return HK_OK;
 }

@@ -120,7 +120,9 @@ def lib() -> C.CDLL:
         "hk_scene_upload": (i32, [vp, C.POINTER(hk_scene_desc)]),
         "hk_set_noise": (i32, [vp, vp, u32, u32]),
         "hk_resize": (i32, [vp, u32, u32, C.c_float, u32, u32]),
-        "hk_band_info": (i32, [vp, C.POINTER(C.c_int32)] * 1 + [C.POINTER(C.c_int32)] * 3),
+        "hk_set_band_halo": (i32, [vp, u32]),
+        "hk_band_info": (i32, [vp] + [C.POINTER(C.c_int32)] * 4),
+        "hk_copy_output_rows": (i32, [vp, i32, u32, u32, vp, i32, vp]),
         "hk_render_gbuffer": (i32, [vp, C.POINTER(hk_frame_inputs), vp]),
         "hk_set_gbuffer_plane": (i32, [vp, i32, vp, C.c_size_t, i32, vp]),
         "hk_render_frame": (i32, [vp, C.POINTER(hk_settings), C.POINTER(hk_frame_inputs), vp]),
@@ -156,7 +158,7 @@ def lib() -> C.CDLL:
 # symbols include/*.h declare (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
-    "hk_set_noise", "hk_resize", "hk_band_info", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
+    "hk_set_noise", "hk_resize", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
     "hk_trace", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",

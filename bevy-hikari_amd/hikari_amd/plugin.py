@@ -64,6 +64,14 @@ class HikariRenderer:
         _check(self.ctx, self._L.hk_resize(self.ctx, width, height, ratio, band_y0, band_rows), "hk_resize")
         self.width, self.height = width, height
 
+    def set_band_halo(self, rows: int) -> None:
+        _check(self.ctx, self._L.hk_set_band_halo(self.ctx, rows), "hk_set_band_halo")
+
+    def copy_output_rows(self, output_id: int, row0: int, rows: int, dst_ptr: int, to_host: bool = False,
+                         stream=None) -> None:
+        _check(self.ctx, self._L.hk_copy_output_rows(self.ctx, output_id, row0, rows, dst_ptr, int(to_host), stream),
+               "hk_copy_output_rows")
+
     def band_info(self):
         v = [C.c_int32() for _ in range(4)]
         _check(self.ctx, self._L.hk_band_info(self.ctx, *[C.byref(x) for x in v]), "hk_band_info")

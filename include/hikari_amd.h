@@ -171,6 +171,10 @@ int hk_set_noise(hk_ctx* ctx, const uint8_t* rgba8, uint32_t count, uint32_t siz
 int hk_resize(hk_ctx* ctx, uint32_t width, uint32_t height, float upscale_ratio,
               uint32_t band_y0, uint32_t band_rows);
 
+/* rows of halo recomputed above and below a band by hk_resize (default 40, enough for spatial
+ * reuse + 4 a-trous levels + the variance blur: 20 + 15 + 1); 0 is exact when spatial reuse and
+ * denoise are both off.  Call before hk_resize. */
+int hk_set_band_halo(hk_ctx* ctx, uint32_t rows);
 /* band geometry after hk_resize: local rows [0, rows) hold global rows [row0, row0+rows);
  * the band's own (non-halo) rows are local [core_row0, core_row0+core_rows) */
 int hk_band_info(const hk_ctx* ctx, int32_t* row0, int32_t* rows, int32_t* core_row0, int32_t* core_rows);
@@ -192,6 +196,10 @@ int hk_output_info(const hk_ctx* ctx, int output_id, uint32_t* width, uint32_t* 
 /* rows [row0, row0+rows) of the plane (rows = 0 => all) */
 int hk_get_output(hk_ctx* ctx, int output_id, void* dst, size_t bytes, int to_host, void* stream);
 const void* hk_output_device_ptr(hk_ctx* ctx, int output_id);
+/* copy band-local rows [row0, row0+rows) of an output plane (e.g. the band's core rows for the
+ * multi-GPU all-gather); dst is host (to_host=1) or device memory */
+int hk_copy_output_rows(hk_ctx* ctx, int output_id, uint32_t row0, uint32_t rows, void* dst, int to_host,
+                        void* stream);
 /* copy reservoir buffer `id` (0..9) in the reference's AoS PackedReservoir layout */
 int hk_dump_reservoirs(hk_ctx* ctx, int id, hk_packed_reservoir* dst, size_t count, void* stream);
 int hk_load_reservoirs(hk_ctx* ctx, int id, const hk_packed_reservoir* src, size_t count, void* stream);
