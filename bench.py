@@ -33,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
+from hikari_amd.bands import band_of, halo_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -143,17 +144,15 @@ def main():
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
     s = st.to_c()
 
-    # row band of this rank
-    assert H % world == 0, "frame height must divide evenly into bands"
-    band = H // world
-    y0 = rank * band
+    # row band of this rank (hikari_amd/bands.py)
+    b = band_of(rank, world, H)
+    band = b.rows
     r = HikariRenderer(local)
     r.set_noise()
     r.upload_scene(scene)
-    needs_halo = cfg["spatial"] or cfg["denoise"]
-    r.set_band_halo(40 if needs_halo else 0)
+    r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
     if world > 1:
-        r.resize(W, H, 1.0, y0, band)
+        r.resize(W, H, 1.0, b.y0, b.rows)
     else:
         r.resize(W, H, 1.0)
     row0, rows, core0, core_rows = r.band_info()

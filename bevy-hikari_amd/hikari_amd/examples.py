@@ -80,9 +80,9 @@ def box_grid_mesh(mn, mx, triangles: int, rng: np.random.Generator) -> Mesh:
                 np.array(idx[: 3 * triangles], np.uint32))
 
 
-def city_proxy(scene: Scene, root: np.ndarray, scale: float = 1.0) -> int:
-    """Add the City glTF node graph with proxy meshes (exact per-mesh triangle counts, AABBs,
-    transforms, emissive factors from assets/models/City/scene.gltf). Returns traced triangles."""
+def city_proxy_assets(scene: Scene):
+    """Mesh + material assets of the City glTF proxy (exact per-mesh triangle counts, AABBs and
+    emissive factors from assets/models/City/scene.gltf); returns a handle for city_proxy_spawn."""
     layout = json.loads((ASSETS / "city_layout.json").read_text())
     rng = np.random.default_rng(PROXY_SEED)
     mats = []
@@ -91,7 +91,6 @@ def city_proxy(scene: Scene, root: np.ndarray, scale: float = 1.0) -> int:
         mats.append(scene.add_material(StandardMaterial(base_color=tuple(m["base_color"]), emissive=(e[0], e[1], e[2], 1.0),
                                                         perceptual_roughness=m["roughness"], metallic=m["metallic"])))
     mesh_ids = []
-    tris = 0
     for prims in layout["meshes"]:
         ids = []
         for p in prims:
@@ -99,25 +98,36 @@ def city_proxy(scene: Scene, root: np.ndarray, scale: float = 1.0) -> int:
                 ids.append(None)
                 continue
             t = p["index_count"] // 3
-            ids.append((scene.add_mesh(box_grid_mesh(p["min"], p["max"], t, rng)), mats[p["material"]]))
+            ids.append((scene.add_mesh(box_grid_mesh(p["min"], p["max"], t, rng)), mats[p["material"]], t))
         mesh_ids.append(ids)
+    return layout, mesh_ids
+
+
+def city_proxy_spawn(scene: Scene, assets, root: np.ndarray, scale: float = 1.0) -> int:
+    """Spawn one SceneBundle of the proxy (instances in node DFS order). Returns traced triangles."""
+    layout, mesh_ids = assets
     S = np.diag([scale, scale, scale, 1.0])
+    tris = 0
 
     def visit(ni, parent):
         nonlocal tris
         n = layout["nodes"][ni]
         world = parent @ _node_matrix(n)
         if "mesh" in n:
-            for entry, p in zip(mesh_ids[n["mesh"]], layout["meshes"][n["mesh"]]):
+            for entry in mesh_ids[n["mesh"]]:
                 if entry is not None:
                     scene.add_instance(entry[0], entry[1], world)
-                    tris += p["index_count"] // 3
+                    tris += entry[2]
         for c in n.get("children", []):
             visit(c, world)
 
     for r in layout["scene_roots"]:
         visit(r, np.asarray(root, np.float64) @ S)
     return tris
+
+
+def city_proxy(scene: Scene, root: np.ndarray, scale: float = 1.0) -> int:
+    return city_proxy_spawn(scene, city_proxy_assets(scene), root, scale)
 
 
 def _emissive_sphere(scene: Scene, translation) -> None:
@@ -151,8 +161,9 @@ def city():
     slots = [(4.0 * l, 0.0, 0.0) for l in (-3, -1, 1, 3)]
     slots += [(4.0 * l, 0.0, 8.0 * (1.0 if i % 2 == 0 else -1.0)) for i, l in enumerate((-3, -1, 1, 3))]
     slots += [(4.0 * l, 0.0, 8.0 * (-1.0 if i % 2 == 0 else 1.0)) for i, l in enumerate((-3, -1, 1, 3))]
+    assets = city_proxy_assets(scene)  # one asset set, 12 spawns (like one glb handle)
     for s in slots:
-        city_proxy(scene, Transform(np.asarray(s, np.float64)).matrix(), scale=0.0005)
+        city_proxy_spawn(scene, assets, Transform(np.asarray(s, np.float64)).matrix(), scale=0.0005)
     sun = DirectionalLight(illuminance=10000.0,
                            transform=Transform(np.array([0.0, 5.0, 0.0]), quat_from_euler_xyz(-math.pi / 4, math.pi / 4, 0)))
     camera = Camera(Transform.from_xyz(-20.0, 10.0, 20.0).looking_at((0.0, 0.0, 0.0)))

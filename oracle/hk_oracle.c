@@ -145,6 +145,7 @@ struct hko_ctx {
     uint16_t* denoised[3];
     uint16_t* tone;
     hk_counters counters;
+    int32_t band_y0, band_y1; /* rows computed by every pass (whole frame by default) */
 };
 
 typedef struct {
@@ -1635,6 +1636,8 @@ hko_ctx* hko_create(const hk_scene_desc* sc, const uint8_t* noise, uint32_t widt
     c->s[0] = (uint32_t)ceilf((1.0f / ratio) * (float)width);
     c->s[1] = (uint32_t)ceilf((1.0f / ratio) * (float)height);
     c->threads = threads;
+    c->band_y0 = 0;
+    c->band_y1 = (int32_t)height;
     size_t S = (size_t)width * height, s = (size_t)c->s[0] * c->s[1];
     c->g_position = (float*)calloc(S * 4, sizeof(float));
     c->g_normal = (uint32_t*)calloc(S, sizeof(uint32_t));
@@ -1689,7 +1692,7 @@ void hko_render_gbuffer(hko_ctx* c, const hk_frame_inputs* in)
     {
         Counts k = {0, 0, 0};
 #pragma omp for schedule(dynamic, 4)
-        for (int32_t y = 0; y < (int32_t)c->S[1]; ++y)
+        for (int32_t y = c->band_y0; y < c->band_y1; ++y)
             for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) gbuffer_pixel(c, &k, in, x, y);
         add_counts(c, &k);
     }
@@ -1703,7 +1706,7 @@ static void run_pass(hko_ctx* c, const Pass* P, Kind kind)
     {
         Counts k = {0, 0, 0};
 #pragma omp for schedule(dynamic, 4)
-        for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
+        for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
             for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) {
                 if (kind == K_DIRECT) direct_lit(P, &k, x, y);
                 else if (kind == K_INDIRECT) indirect_lit_ambient(P, &k, x, y);
@@ -1724,7 +1727,7 @@ void hko_render_frame(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* 
     P.number = in->frame_number;
     /* full-screen albedo over S */
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
-    for (int32_t y = 0; y < (int32_t)c->S[1]; ++y)
+    for (int32_t y = c->band_y0; y < c->band_y1; ++y)
         for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) full_screen_albedo(&P, x, y);
 
     uint32_t current = P.number % 2u, previous = 1u - current;
@@ -1771,12 +1774,12 @@ void hko_denoise(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
         D.out = c->denoised[ch];
         D.level = 0;
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
-        for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
+        for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
             for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) demodulation(&D, x, y);
         for (int level = 0; level < 4; ++level) {
             D.level = level;
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
-            for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
+            for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
                 for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) denoise_pixel(&D, x, y);
         }
     }
@@ -1840,6 +1843,13 @@ hk_packed_reservoir* hko_reservoirs(hko_ctx* c, int id, uint32_t* count)
     if (id < 0 || id >= HK_RESERVOIR_BUFFERS) return NULL;
     if (count) *count = c->S[0] * c->S[1];
     return c->reservoirs[id];
+}
+
+void hko_set_band(hko_ctx* c, int32_t y0, int32_t rows, int32_t halo)
+{
+    int32_t a = y0 - halo, b = y0 + rows + halo;
+    c->band_y0 = a < 0 ? 0 : a;
+    c->band_y1 = b > (int32_t)c->S[1] ? (int32_t)c->S[1] : b;
 }
 
 void hko_counters(hko_ctx* c, hk_counters* out) { *out = c->counters; }

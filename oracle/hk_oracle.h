@@ -32,6 +32,8 @@ typedef struct hko_ctx hko_ctx;
 hko_ctx* hko_create(const hk_scene_desc* scene, const uint8_t* noise, uint32_t width, uint32_t height,
                     float upscale_ratio, int threads);
 void hko_destroy(hko_ctx* ctx);
+/* restrict every pass to rows [y0 - halo, y0 + rows + halo) (multi-rank band tests; ratio 1) */
+void hko_set_band(hko_ctx* ctx, int32_t y0, int32_t rows, int32_t halo);
 
 void hko_render_gbuffer(hko_ctx* ctx, const hk_frame_inputs* inputs);
 void hko_render_frame(hko_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs);

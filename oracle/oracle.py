@@ -33,6 +33,7 @@ def lib() -> C.CDLL:
     sigs = {
         "hko_create": (vp, [vp, vp, u32, u32, f, C.c_int]),
         "hko_destroy": (None, [vp]),
+        "hko_set_band": (None, [vp, C.c_int32, C.c_int32, C.c_int32]),
         "hko_render_gbuffer": (None, [vp, vp]),
         "hko_render_frame": (None, [vp, vp, vp]),
         "hko_denoise": (None, [vp, vp, vp]),
@@ -79,6 +80,9 @@ class Oracle:
 
     def __del__(self):
         self.close()
+
+    def set_band(self, y0: int, rows: int, halo: int = 40):
+        self._L.hko_set_band(self.ctx, y0, rows, halo)
 
     def render_gbuffer(self, inputs):
         self._L.hko_render_gbuffer(self.ctx, C.byref(inputs))

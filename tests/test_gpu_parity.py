@@ -83,3 +83,114 @@ def test_trace_matches_oracle():
     b = o.trace(rays, None, early, excl)
     assert (a == b).all(), f"{int((a != b).any(axis=1).sum())} of {n} rays differ"
     assert (a[:, 3] != 0xFFFFFFFF).mean() > 0.5
+
+
+@pytest.mark.parametrize("spatial,denoise", [(True, True), (False, False)])
+def test_gpu_row_bands_match_whole_frame(spatial, denoise):
+    """Two band contexts (the multi-GPU decomposition, run on one GPU) reproduce the
+    whole-frame oracle render bit-exactly on their own rows, and count only their own rays."""
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
+    from hikari_amd.bands import band_of, halo_rows
+    from oracle import Oracle
+    W, H = 64, 96
+    scene, cam, lights = examples.cornell()
+    desc = scene.build()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=spatial, denoise=denoise)
+    s = st.to_c()
+    o = Oracle(desc, load_noise(), W, H, 1.0)
+    ranks = []
+    for k in range(2):
+        b = band_of(k, 2, H)
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.set_band_halo(halo_rows(spatial, denoise))
+        r.resize(W, H, 1.0, b.y0, b.rows)
+        ranks.append((b, r))
+    for f in range(5):
+        fi = frame_inputs(f, cam, lights, W, H)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.denoise(s, fi)
+        o.tone_sum(s)
+        for b, r in ranks:
+            r.render_gbuffer(fi)
+            r.render_frame(s, fi)
+            r.denoise(s, fi)
+            r.tone_sum(s)
+    whole = o.output(10)
+    total = {"traverse_top": 0, "traverse_emitter": 0, "primary": 0}
+    for b, r in ranks:
+        row0, rows, core0, core_rows = r.band_info()
+        assert row0 + core0 == b.y0 and core_rows == b.rows
+        mine = r.output(10)[core0: core0 + core_rows]
+        assert np.array_equal(canon_plane(10, mine), canon_plane(10, whole[b.y0: b.y0 + b.rows])), b
+        for k, v in r.counters().items():
+            total[k] += v
+    assert total == o.counters()
+
+
+def _gpu_factory(w, h, ratio=1.0):
+    def make(scene, desc):
+        from hikari_amd import HikariRenderer
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.resize(w, h, ratio)
+        return r
+    return make
+
+
+@pytest.mark.parametrize("variant", ["default_ratio1", "emissive_spatial_multibounce", "no_temporal_no_spatial",
+                                     "no_indirect", "validate_every_frame"])
+def test_gpu_matches_golden_digests(variant):
+    """GPU renders of the committed golden variants (tests/golden/) reproduce every digest."""
+    import json
+    from pathlib import Path
+
+    import make_golden_path  # noqa: F401
+    from make_golden import FRAMES, H, W, render
+    gold = json.loads((Path(__file__).parent / "golden" / "cornell_golden.json").read_text())
+    frames, _ = render(_gpu_factory(W, H), variant)
+    for f, (a, b) in enumerate(zip(frames, gold["variants"][variant]["digests"])):
+        bad = [k for k in b if a[k] != b[k]]
+        assert not bad, f"{variant} frame {f}: {bad}"
+
+
+def _run_pair(scene_fn, w, h, settings, frames):
+    from hikari_amd import HikariRenderer, examples, frame_inputs, load_noise
+    from oracle import Oracle
+    scene, cam, lights = examples.SCENES[scene_fn]()
+    desc = scene.build()
+    ratio = settings.upscale.ratio()
+    r = _gpu_factory(w, h, ratio)(scene, desc)
+    o = Oracle(desc, load_noise(), w, h, ratio)
+    s = settings.to_c()
+    errors = []
+    for f in range(frames):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        _compare_frame(r, o, f, errors)
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
+    assert r.counters() == o.counters()
+    return r, o
+
+
+def test_upscale_ratio_two_half_resolution_integrator():
+    """SMAA_TU_2_0 (the default): integrator at s = ceil(S/2), jittered deferred lookups."""
+    from hikari_amd import HikariSettings, Upscale
+    _run_pair("cornell", 64, 48, HikariSettings(upscale=Upscale.SMAA_TU_2_0), 5)
+
+
+@pytest.mark.parametrize("scene_fn,size", [("scene", (64, 40)), ("city", (48, 32))])
+def test_proxy_scenes_with_directional_light(scene_fn, size):
+    """City-proxy scenes: 140K-triangle BLASes, a directional light (cone sampling, any-hit
+    shadow rays) and an emissive sphere."""
+    from hikari_amd import HikariSettings, Upscale
+    _run_pair(scene_fn, size[0], size[1], HikariSettings(upscale=Upscale.SMAA_TU_1_0), 4)
