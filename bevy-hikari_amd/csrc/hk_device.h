@@ -123,7 +123,8 @@ struct Frame {
     uint32_t S[2], s[2];
     int32_t S_row0, S_rows;  // deferred-plane band
     int32_t s_row0, s_rows;  // integrator-plane band
-    int32_t count_y0, count_y1;  // global rows whose rays are counted (the band's own rows)
+    int32_t count_y0, count_y1;    // global integrator rows whose rays are counted (the band's own rows)
+    int32_t count_Sy0, count_Sy1;  // the same for the full-resolution G-buffer rows
 };
 
 // Row-major planes of the deferred (G-buffer) textures, band-local.

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V)
             A.G.velocity_uv[idx] = make_float4(0.0f, 0.0f, info.uv.x, info.uv.y);
         }
     }
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_primary = 0;
+    if (y < A.F.count_Sy0 || y >= A.F.count_Sy1) n_primary = 0;
     wave_count(A.cnt.primary, n_primary);
 }
 

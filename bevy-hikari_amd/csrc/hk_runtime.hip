@@ -225,6 +225,10 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     F.s_rows = c->s_rows;
     F.count_y0 = c->s_row0 + c->core_row0;
     F.count_y1 = F.count_y0 + c->core_rows;
+    // G-buffer rows: whole frame, or (ratio 1 bands) the same rows as the integrator
+    F.count_Sy0 = c->S_row0 + c->core_row0;
+    F.count_Sy1 = c->S_rows == (int32_t)c->S[1] && c->core_rows == (int32_t)c->s[1] ? (int32_t)c->S[1]
+                                                                                      : F.count_Sy0 + c->core_rows;
     A.G.position = c->g_position;
     A.G.normal = c->g_normal;
     A.G.depth_gradient = c->g_depth_gradient;
