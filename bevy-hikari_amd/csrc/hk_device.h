@@ -882,13 +882,18 @@ HKD f4 noise_random(const uchar4* noise, uint32_t number, int32_t x, int32_t y)
                hk_fract((float)t.w / 255.0f + fn));
 }
 
-// wave-aggregated 64-bit counter add (one atomic per wave)
+// Ray counters are sharded: COUNTER_SHARDS 64-byte lines per counter, each wave adds its
+// wave-reduced count to the line of its workgroup's shard.  A single shared word would
+// serialise tens of thousands of same-address atomics per kernel at the memory side.
+constexpr uint32_t COUNTER_SHARDS = 1024;
+constexpr uint32_t COUNTER_STRIDE = 8;  // u64 per shard line (64 B)
 HKD void wave_count(unsigned long long* dst, uint32_t v)
 {
     unsigned long long s = v;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
+    uint32_t shard = ((blockIdx.x + blockIdx.y * gridDim.x) * 4u + (threadIdx.x >> 6)) % COUNTER_SHARDS;
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(dst + (size_t)shard * COUNTER_STRIDE, s);
 }
 
 }  // namespace hk

@@ -22,7 +22,10 @@
 using namespace hk;
 
 namespace {
-constexpr int32_t BAND_HALO = 40;  // >= 36 rows: 20 (spatial reuse) + 15 (a-trous) + 1 (variance blur)
+constexpr int32_t BAND_HALO = 40;
+// 3 counters (top, emitter, primary) x COUNTER_SHARDS lines of 64 B
+constexpr size_t COUNTER_SPAN = (size_t)COUNTER_SHARDS * COUNTER_STRIDE;  // u64 per counter
+constexpr size_t COUNTER_BYTES = 3 * COUNTER_SPAN * sizeof(unsigned long long);  // >= 36 rows: 20 (spatial reuse) + 15 (a-trous) + 1 (variance blur)
 
 struct TimedLaunch {
     const char* name;
@@ -236,8 +239,8 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.G.velocity_uv = c->g_velocity_uv;
     A.noise = c->noise;
     A.cnt.top = c->counters;
-    A.cnt.emitter = c->counters + 1;
-    A.cnt.primary = c->counters + 2;
+    A.cnt.emitter = c->counters + COUNTER_SPAN;
+    A.cnt.primary = c->counters + 2 * COUNTER_SPAN;
     return A;
 }
 
@@ -292,8 +295,7 @@ int hk_create(int device, hk_ctx** out)
     hk_ctx* c = new hk_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->counters, COUNTER_BYTES) != hipSuccess || hipMemset(c->counters, 0, COUNTER_BYTES) != hipSuccess) {
         delete c;
         return HK_ERR_HIP;
     }
@@ -688,7 +690,7 @@ int hk_reset_counters(hk_ctx* c, void* stream)
 {
     if (!c) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
-    HK_HIP(c, hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), pick(c, stream)));
+    HK_HIP(c, hipMemsetAsync(c->counters, 0, COUNTER_BYTES, pick(c, stream)));
     return HK_OK;
 }
 
@@ -697,12 +699,15 @@ int hk_read_counters(hk_ctx* c, hk_counters* out, void* stream)
     if (!c || !out) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
-    unsigned long long v[4];
-    HK_HIP(c, hipMemcpyAsync(v, c->counters, sizeof(v), hipMemcpyDeviceToHost, st));
+    std::vector<unsigned long long> v(3 * COUNTER_SPAN);
+    HK_HIP(c, hipMemcpyAsync(v.data(), c->counters, COUNTER_BYTES, hipMemcpyDeviceToHost, st));
     HK_HIP(c, hipStreamSynchronize(st));
-    out->traverse_top = v[0];
-    out->traverse_emitter = v[1];
-    out->primary = v[2];
+    unsigned long long sum[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k)
+        for (size_t i = 0; i < COUNTER_SHARDS; ++i) sum[k] += v[k * COUNTER_SPAN + i * COUNTER_STRIDE];
+    out->traverse_top = sum[0];
+    out->traverse_emitter = sum[1];
+    out->primary = sum[2];
     return HK_OK;
 }
 
