@@ -47,9 +47,8 @@ BYTES_PER_PIXEL = {
     "indirect_multiple_bounces": 184,
     "indirect_spatial_reuse": 244,   # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8
     "emissive_spatial_reuse": 244,
-    "demodulation": 32,
-    "denoise": 56,
-    "denoise_firefly": 56,
+    "demodulation": 92,              # 3 channels x (render 8 + variance 4 + internal 8 + ivar 4) + albedo 8 + G 12 + geom 32
+    "denoise": 120,                  # geom 32 + 3 x (ivar 4 + input 8 + output 8) (+ albedo 8 at L3)
     "tone_mapping": 32,
 }
 
@@ -208,7 +207,7 @@ def main():
         # roofline of the dominant kernel (largest total time per frame)
         per_frame = {}
         for name, avg in timing.items():
-            launches = {"denoise": 4, "denoise_firefly": 8, "demodulation": 3 if st.indirect_bounces else 2}.get(name, 1)
+            launches = {"denoise": 4}.get(name, 1)
             per_frame[name] = avg * launches
         dom = max(per_frame, key=per_frame.get)
         pix = W * rows

@@ -787,38 +787,64 @@ HKD f3 EnvBRDFApprox(f3 f0, float pr, float NoV)
     float ABy = 1.04f * a004 + rw;
     return mk3(f0.x * ABx + ABy, f0.y * ABx + ABy, f0.z * ABx + ABy);
 }
-HKD f3 lit(f3 radiance, f3 diffuse_color, float roughness, f3 F0, f3 L, f3 N, f3 V)
+// shading() (light.wgsl:869-888) split into the part that depends only on (V, N, surface) —
+// evaluated once per pixel — and the per-light part.  Every expression is the one lit()/
+// ambient() evaluate (Bevy PBR), in the same order, so results are bit-identical
+// to calling shading() each time; spatial reuse calls it up to 18 times per pixel.
+struct ShadeCtx {
+    f3 V, N, F0, diffuse_color, ambient;
+    float roughness, NdotV, pow5_view, smith_view;
+};
+HKD ShadeCtx shade_ctx(const Frame& F, f3 V, f3 N, const Surface& s)
 {
-    f3 H = normalize(L + V);
-    float NoL = hk_saturate(dot(N, L));
-    float NoH = hk_saturate(dot(N, H));
+    ShadeCtx c;
+    c.V = V;
+    c.N = N;
+    f3 base = xyz(s.base_color);
+    float f0s = ((0.16f * s.reflectance) * s.reflectance) * (1.0f - s.metallic);
+    c.F0 = mk3(f0s + base.x * s.metallic, f0s + base.y * s.metallic, f0s + base.z * s.metallic);
+    c.diffuse_color = base * (1.0f - s.metallic);
+    c.roughness = s.roughness;
+    c.NdotV = fmaxf(dot(N, V), 0.0001f);
+    c.pow5_view = hk_pow(1.0f - c.NdotV, 5.0f);  // F_Schlick(1, f90, NdotV) of Fd_Burley
+    float a2 = s.roughness * s.roughness;
+    c.smith_view = sqrtf((c.NdotV - a2 * c.NdotV) * c.NdotV + a2);  // lambdaV's root
+    // ambient() (light.wgsl:820-833)
+    f3 da = EnvBRDFApprox(c.diffuse_color, 1.0f, c.NdotV);
+    f3 sa = EnvBRDFApprox(c.F0, s.roughness, c.NdotV);
+    c.ambient = ((da + sa) * s.occlusion) * ld3(F.ambient_color);
+    return c;
+}
+HKD f3 shade(const ShadeCtx& c, f3 L, f4 in_radiance)
+{
+    // lit() (light.wgsl:796-818)
+    f3 H = normalize(L + c.V);
+    float NoL = hk_saturate(dot(c.N, L));
+    float NoH = hk_saturate(dot(c.N, H));
     float LoH = hk_saturate(dot(L, H));
-    float NdotV = fmaxf(dot(N, V), 0.0001f);
-    // Fd_Burley
+    float roughness = c.roughness;
     float f90 = 0.5f + ((2.0f * roughness) * LoH) * LoH;
-    float fd = (F_Schlick(1.0f, f90, NoL) * F_Schlick(1.0f, f90, NdotV)) * (1.0f / HK_PI);
-    f3 diffuse = diffuse_color * fd;
-    // specular = D_GGX * V_SmithGGXCorrelated * fresnel
+    float fd = (F_Schlick(1.0f, f90, NoL) * (1.0f + (f90 - 1.0f) * c.pow5_view)) * (1.0f / HK_PI);
+    f3 diffuse = c.diffuse_color * fd;
     float one_minus = 1.0f - NoH * NoH;
     float a = NoH * roughness;
     float k = roughness / (one_minus + a * a);
     float D = (k * k) * (1.0f / HK_PI);
     float a2 = roughness * roughness;
-    float lambdaV = NoL * sqrtf((NdotV - a2 * NdotV) * NdotV + a2);
-    float lambdaL = NdotV * sqrtf((NoL - a2 * NoL) * NoL + a2);
+    float lambdaV = NoL * c.smith_view;
+    float lambdaL = c.NdotV * sqrtf((NoL - a2 * NoL) * NoL + a2);
     float Vis = 0.5f / (lambdaV + lambdaL);
-    float fr90 = hk_saturate(dot(F0, mk3(16.5f, 16.5f, 16.5f)));
-    f3 F = F_Schlick_vec(F0, fr90, LoH);
-    f3 specular_light = F * ((1.0f * D) * Vis);
-    return ((specular_light + diffuse) * radiance) * NoL;
+    float fr90 = hk_saturate(dot(c.F0, mk3(16.5f, 16.5f, 16.5f)));
+    f3 Fr = F_Schlick_vec(c.F0, fr90, LoH);
+    f3 specular_light = Fr * ((1.0f * D) * Vis);
+    f3 lit_radiance = ((specular_light + diffuse) * xyz(in_radiance)) * NoL;
+    return mix(lit_radiance, c.ambient, 1.0f - in_radiance.w);
 }
-HKD f3 ambient(const Frame& F, f3 diffuse_color, float roughness, float occlusion, f3 F0, f3 N, f3 V)
+HKD f3 shading(const Frame& F, f3 V, f3 N, f3 L, const Surface& s, f4 in_radiance)
 {
-    float NdotV = fmaxf(dot(N, V), 0.0001f);
-    f3 da = EnvBRDFApprox(diffuse_color, 1.0f, NdotV);
-    f3 sa = EnvBRDFApprox(F0, roughness, NdotV);
-    return ((da + sa) * occlusion) * ld3(F.ambient_color);
+    return shade(shade_ctx(F, V, N, s), L, in_radiance);
 }
+// light.wgsl:835-867
 HKD f4 input_radiance(const Scene& sc, const Frame& F, const Ray& ray, const HitInfo& info, bool sample_directional,
                       uint32_t sample_emissive, bool sample_ambient)
 {
@@ -837,16 +863,6 @@ HKD f4 input_radiance(const Scene& sc, const Frame& F, const Ray& ray, const Hit
         radiance = emissive_radiance(retreive_emissive(sc, info.material_index));
     }
     return mk4(radiance.x, radiance.y, radiance.z, 1.0f - amb);
-}
-HKD f3 shading(const Frame& F, f3 V, f3 N, f3 L, const Surface& s, f4 in_radiance)
-{
-    f3 base = xyz(s.base_color);
-    float f0s = ((0.16f * s.reflectance) * s.reflectance) * (1.0f - s.metallic);
-    f3 F0 = mk3(f0s + base.x * s.metallic, f0s + base.y * s.metallic, f0s + base.z * s.metallic);
-    f3 diffuse_color = base * (1.0f - s.metallic);
-    f3 lr = lit(xyz(in_radiance), diffuse_color, s.roughness, F0, L, N, V);
-    f3 ar = ambient(F, diffuse_color, s.roughness, s.occlusion, F0, N, V);
-    return mix(lr, ar, 1.0f - in_radiance.w);
 }
 HKD f3 env_brdf(f3 V, f3 N, const Surface& s)
 {

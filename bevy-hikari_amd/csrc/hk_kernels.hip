@@ -5,8 +5,8 @@
 //   light.wgsl:1044 direct_lit (+RENDER_EMISSIVE / +EMISSIVE_LIT) -> k_direct<EMISSIVE_LIT, RENDER_EMISSIVE>
 //   light.wgsl:1263 indirect_lit_ambient (+MULTIPLE_BOUNCES)      -> k_indirect<MULTI>
 //   light.wgsl:1503 spatial_reuse (+EMISSIVE_LIT)                 -> k_spatial<EMISSIVE_LIT>
-//   denoise.wgsl:135 demodulation                                 -> k_demod
-//   denoise.wgsl:215 denoise (DENOISE_LEVEL_0..3, FIREFLY)        -> k_denoise<FIREFLY>
+//   denoise.wgsl:135 demodulation (x3 channels)                   -> k_demod3<C>
+//   denoise.wgsl:215 denoise (DENOISE_LEVEL_0..3, FIREFLY) x3 ch  -> k_denoise3<C, LEVEL>
 //   tone_mapping.wgsl:21 tone_mapping                             -> k_tone
 //   prepass.wgsl:84-100 (raster G-buffer)                         -> k_gbuffer (primary rays)
 //   light.wgsl:442 traverse_top                                   -> k_trace
@@ -452,11 +452,11 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     float lifetime_max = F.max_reservoir_lifetime <= 1.0f ? HK_F32_MAX : F.max_reservoir_lifetime;
     if (r.lifetime <= lifetime_max) r = load_previous(F, C.prev_spatial, previous_uv);
     f3 view_direction = calculate_view(F, position);
+    const ShadeCtx sc = shade_ctx(F, view_direction, s.visible_normal, surface);
     if (EMISSIVE_LIT) {
         merge_reservoir(r, q, lum(xyz(q.s.radiance)));
     } else {
-        f3 o = shading(F, view_direction, s.visible_normal, normalize(xyz(s.sample_position) - xyz(s.visible_position)),
-                       surface, s.radiance);
+        f3 o = shade(sc, normalize(xyz(s.sample_position) - xyz(s.visible_position)), s.radiance);
         merge_reservoir(r, q, lum(o));
     }
     r.s.visible_position = s.visible_position;
@@ -506,7 +506,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         if (EMISSIVE_LIT) {
             merge_reservoir(r, q, lum(xyz(q.s.radiance)) / jacobian);
         } else {
-            f3 o = shading(F, view_direction, s.visible_normal, sample_direction, surface, q.s.radiance);
+            f3 o = shade(sc, sample_direction, q.s.radiance);
             merge_reservoir(r, q, lum(o) / jacobian);
         }
     }
@@ -516,8 +516,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         r.w2_sum *= m / r.count;
         r.count = m;
     }
-    f3 out = shading(F, view_direction, s.visible_normal, normalize(xyz(r.s.sample_position) - xyz(s.visible_position)),
-                     surface, r.s.radiance);
+    f3 out = shade(sc, normalize(xyz(r.s.sample_position) - xyz(s.visible_position)), r.s.radiance);
     float total_lum = EMISSIVE_LIT ? r.count * lum(xyz(r.s.radiance)) : r.count * lum(out);
     r.w = total_lum > 0.0f ? r.w_sum / total_lum : 0.0f;
     r.lifetime += 1.0f;
@@ -548,7 +547,20 @@ HKD f4 load_albedo(const Frame& F, const uint2* albedo, int32_t x, int32_t y)
     return load_rgba16f(albedo, band_index(x, y, F.S[0], F.S_row0, F.S_rows));
 }
 
-__global__ __launch_bounds__(256) void k_demod(FrameArgs A, DenoiseArgs D)
+// Channel-fused denoiser.  The reference runs demodulation + 4 levels separately for each
+// of the 3 channels (post_process.rs:1199-1223); channels are independent and share every
+// geometry weight, so one launch per level processes all channels and computes the normal /
+// depth / instance weights of each tap once.  The per-pixel geometry (normalised normal,
+// depth, instance, depth gradient at the pixel's deferred texel) is produced once per frame
+// by k_demod3 with exactly the expressions denoise.wgsl evaluates per tap.
+HKD void store_geom(const DenoiseArgs& D, int32_t idx, f3 n, float depth, float inst, f2 grad)
+{
+    D.geom[2 * idx] = make_float4(n.x, n.y, n.z, depth);
+    D.geom[2 * idx + 1] = make_float4(inst, grad.x, grad.y, 0.0f);
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
@@ -558,102 +570,118 @@ __global__ __launch_bounds__(256) void k_demod(FrameArgs A, DenoiseArgs D)
     f2 duv = jittered_uv(F, uv, 0.5f);
     int32_t ax, ay, rx, ry;
     nearest_texel(duv, F.S, ax, ay);
+    // geometry the denoise levels read for this pixel (denoise.wgsl:220-223, 197-200)
+    store_geom(D, idx, normalize(load_normal(F, A.G, ax, ay)), load_depth(F, A.G, ax, ay),
+               load_instance_material(F, A.G, ax, ay).x, load_depth_gradient(F, A.G, ax, ay));
     f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
     nearest_texel(uv, F.s, rx, ry);
-    f3 irr = xyz(load_rgba16f(D.render, s_index(F, rx, ry)));
-    irr = mk3(albedo.x < 0.01f ? 0.0f : irr.x / albedo.x, albedo.y < 0.01f ? 0.0f : irr.y / albedo.y,
-              albedo.z < 0.01f ? 0.0f : irr.z / albedo.z);
-    store_rgba16f(D.internal[0], idx, mk4(irr.x, irr.y, irr.z, 1.0f));
-    float sum_variance = 0.0f;
+    const int32_t ridx = s_index(F, rx, ry);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const int ox = k / 3 - 1, oy = k % 3 - 1;  // (-1,-1),(-1,0),(-1,1),(0,-1),...
-        f2 suv = mk2(uv.x + (float)ox / (float)F.s[0], uv.y + (float)oy / (float)F.s[1]);
-        if (uv_outside(suv)) continue;
-        int32_t vx, vy;
-        nearest_texel(suv, F.s, vx, vy);
-        float v = D.variance[s_index(F, vx, vy)];
-        if (v > HK_F32_MAX) continue;
-        sum_variance += KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
+    for (int ch = 0; ch < C; ++ch) {
+        f3 irr = xyz(load_rgba16f(D.render[ch], ridx));
+        irr = mk3(albedo.x < 0.01f ? 0.0f : irr.x / albedo.x, albedo.y < 0.01f ? 0.0f : irr.y / albedo.y,
+                  albedo.z < 0.01f ? 0.0f : irr.z / albedo.z);
+        store_rgba16f(D.internal[ch][0], idx, mk4(irr.x, irr.y, irr.z, 1.0f));
+        float sum_variance = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int ox = k / 3 - 1, oy = k % 3 - 1;  // (-1,-1),(-1,0),(-1,1),(0,-1),...
+            f2 suv = mk2(uv.x + (float)ox / (float)F.s[0], uv.y + (float)oy / (float)F.s[1]);
+            if (uv_outside(suv)) continue;
+            int32_t vx, vy;
+            nearest_texel(suv, F.s, vx, vy);
+            float v = D.variance[ch][s_index(F, vx, vy)];
+            if (v > HK_F32_MAX) continue;
+            sum_variance += KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
+        }
+        D.internal_variance[ch][idx] = sum_variance;
     }
-    D.internal_variance[idx] = sum_variance;
 }
 
-template <bool FIREFLY>
-__global__ __launch_bounds__(256) void k_denoise(FrameArgs A, DenoiseArgs D, int level)
+template <int C, int LEVEL>
+__global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
     if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
-    const uint2* input = D.internal[level];
-    uint2* output = level == 3 ? D.output : D.internal[level + 1];
-    const int32_t step = 8 >> level;
-    f2 uv = coords_to_uv(x, y, F.s);
-    f2 duv = jittered_uv(F, uv, 0.5f);
-    int32_t gx, gy;
-    nearest_texel(duv, F.S, gx, gy);
-    float depth = load_depth(F, A.G, gx, gy);
-    f2 depth_gradient = load_depth_gradient(F, A.G, gx, gy);
-    f3 normal = normalize(load_normal(F, A.G, gx, gy));
-    float instance = load_instance_material(F, A.G, gx, gy).x;
+    constexpr int32_t step = 8 >> LEVEL;
+    const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
+    const float depth = g0.w;
     if (depth < HK_F32_EPSILON) {
-        store_rgba16f(output, idx, mk4(0, 0, 0, 0));
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) store_rgba16f(LEVEL == 3 ? D.output[ch] : D.internal[ch][LEVEL + 1], idx, mk4(0, 0, 0, 0));
         return;
     }
-    float variance = D.internal_variance[idx];
-    f3 irradiance = xyz(load_rgba16f(input, idx));
-    f3 sum_irr = irradiance * 0.25f;
-    float sum_w = 0.25f;
-    if (bad3(irradiance)) {
-        irradiance = mk3(0, 0, 0);
-        sum_irr = mk3(0, 0, 0);
-        sum_w = 0.0f;
+    const f3 normal = mk3(g0.x, g0.y, g0.z);
+    const float instance = g1.x;
+    const f2 depth_gradient = mk2(g1.y, g1.z);
+    f3 sum_irr[C], irradiance[C];
+    float sum_w[C], l0[C], lum_denom[C], m1[C], m2[C], cnt[C];
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) {
+        float variance = D.internal_variance[ch][idx];
+        irradiance[ch] = xyz(load_rgba16f(D.internal[ch][LEVEL], idx));
+        sum_irr[ch] = irradiance[ch] * 0.25f;
+        sum_w[ch] = 0.25f;
+        if (bad3(irradiance[ch])) {
+            irradiance[ch] = mk3(0, 0, 0);
+            sum_irr[ch] = mk3(0, 0, 0);
+            sum_w[ch] = 0.0f;
+        }
+        l0[ch] = lum(irradiance[ch]);
+        lum_denom[ch] = 4.0f * hk_pow(variance, 0.25f) + 0.001f;
+        m1[ch] = m2[ch] = cnt[ch] = 0.0f;
     }
-    const float l0 = lum(irradiance);
-    const float lum_denom = 4.0f * hk_pow(variance, 0.25f) + 0.001f;
-    float m1 = 0.0f, m2 = 0.0f, cnt = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int kk = k < 4 ? k : k + 1;  // skip the centre
         const int ox = kk % 3 - 1, oy = kk / 3 - 1;  // (-1,-1),(0,-1),(1,-1),(-1,0),(1,0),(-1,1),(0,1),(1,1)
-        int32_t sx = x + ox * step, sy = y + oy * step;
-        f2 suv = coords_to_uv(sx, sy, F.s);
+        const int32_t sx = x + ox * step, sy = y + oy * step;
+        const f2 suv = coords_to_uv(sx, sy, F.s);
         if (uv_outside(suv)) continue;
-        f3 irr = xyz(load_rgba16f(input, s_index(F, sx, sy)));
-        if (bad3(irr)) continue;
-        f2 sduv = jittered_uv(F, suv, 0.5f);
-        int32_t tx, ty;
-        nearest_texel(sduv, F.S, tx, ty);
-        f3 sn = normalize(load_normal(F, A.G, tx, ty));
-        float sd = load_depth(F, A.G, tx, ty);
-        float si = load_instance_material(F, A.G, tx, ty).x;
-        float sl = lum(irr);
-        float w_normal = hk_pow(fmaxf(0.0f, dot(normal, sn)), 16.0f);
-        float w_depth = hk_exp((-fabsf(depth - sd)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
-        float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
-        float w_lum = hk_exp((-fabsf(l0 - sl)) / lum_denom);
-        float w = hk_clampf(((w_normal * w_depth) * w_instance) * w_lum, 0.0f, 1.0f) * KERNEL3[oy + 1][ox + 1];
-        sum_irr = sum_irr + irr * w;
-        sum_w += w;
-        if (FIREFLY) {
-            m1 += sl;
-            m2 += sl * sl;
-            cnt += 1.0f;
+        const int32_t sidx = s_index(F, sx, sy);
+        const float4 t0 = D.geom[2 * sidx];
+        const float si = D.geom[2 * sidx + 1].x;
+        const float w_normal = hk_pow(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))), 16.0f);
+        const float w_depth = hk_exp((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
+        const float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
+        const float w_geo = (w_normal * w_depth) * w_instance;
+        const float kw = KERNEL3[oy + 1][ox + 1];
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) {
+            f3 irr = xyz(load_rgba16f(D.internal[ch][LEVEL], sidx));
+            if (bad3(irr)) continue;
+            float sl = lum(irr);
+            float w_lum = hk_exp((-fabsf(l0[ch] - sl)) / lum_denom[ch]);
+            float w = hk_clampf(w_geo * w_lum, 0.0f, 1.0f) * kw;
+            sum_irr[ch] = sum_irr[ch] + irr * w;
+            sum_w[ch] += w;
+            if (ch >= 1) {  // FIREFLY_FILTERING on emissive and indirect (post_process.rs:1193-1197)
+                m1[ch] += sl;
+                m2[ch] += sl * sl;
+                cnt[ch] += 1.0f;
+            }
         }
     }
-    irradiance = sum_w < 0.0001f ? mk3(0, 0, 0) : sum_irr / sum_w;
-    if (FIREFLY) {
-        float mean = m1 / cnt;
-        float var = m2 / cnt - mean * mean;
-        if (l0 > mean + 3.0f * sqrtf(var)) irradiance = irradiance * (mean / l0);
+    f4 a = mk4(0, 0, 0, 0);
+    if (LEVEL == 3) {
+        int32_t gx, gy;
+        nearest_texel(jittered_uv(F, coords_to_uv(x, y, F.s), 0.5f), F.S, gx, gy);
+        a = load_albedo(F, D.albedo, gx, gy);
     }
-    f4 color = mk4(irradiance.x, irradiance.y, irradiance.z, 1.0f);
-    if (level == 3) {
-        f4 a = load_albedo(F, D.albedo, gx, gy);
-        color = mk4(color.x * a.x, color.y * a.y, color.z * a.z, color.w * a.w);
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) {
+        f3 ir = sum_w[ch] < 0.0001f ? mk3(0, 0, 0) : sum_irr[ch] / sum_w[ch];
+        if (ch >= 1) {
+            float mean = m1[ch] / cnt[ch];
+            float var = m2[ch] / cnt[ch] - mean * mean;
+            if (l0[ch] > mean + 3.0f * sqrtf(var)) ir = ir * (mean / l0[ch]);
+        }
+        f4 color = mk4(ir.x, ir.y, ir.z, 1.0f);
+        if (LEVEL == 3) color = mk4(color.x * a.x, color.y * a.y, color.z * a.z, color.w * a.w);
+        store_rgba16f(LEVEL == 3 ? D.output[ch] : D.internal[ch][LEVEL + 1], idx, color);
     }
-    store_rgba16f(output, idx, color);
 }
 
 // ------------------------------------------------------------------ tone mapping (tone_mapping.wgsl:21-32)
@@ -733,13 +761,25 @@ void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit,
 }
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_demod, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, D);
+    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    if (D.channels == 3) hipLaunchKernelGGL(k_demod3<3>, g, dim3(256), 0, st, A, D);
+    else hipLaunchKernelGGL(k_demod3<2>, g, dim3(256), 0, st, A, D);
 }
-void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, bool firefly, hipStream_t st)
+template <int C>
+static void launch_level(const FrameArgs& A, const DenoiseArgs& D, int level, dim3 g, hipStream_t st)
+{
+    switch (level) {
+    case 0: hipLaunchKernelGGL((k_denoise3<C, 0>), g, dim3(256), 0, st, A, D); break;
+    case 1: hipLaunchKernelGGL((k_denoise3<C, 1>), g, dim3(256), 0, st, A, D); break;
+    case 2: hipLaunchKernelGGL((k_denoise3<C, 2>), g, dim3(256), 0, st, A, D); break;
+    default: hipLaunchKernelGGL((k_denoise3<C, 3>), g, dim3(256), 0, st, A, D); break;
+    }
+}
+void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st)
 {
     dim3 g = tiles(A.F.s[0], A.F.s_rows);
-    if (firefly) hipLaunchKernelGGL(k_denoise<true>, g, dim3(256), 0, st, A, D, level);
-    else hipLaunchKernelGGL(k_denoise<false>, g, dim3(256), 0, st, A, D, level);
+    if (D.channels == 3) launch_level<3>(A, D, level, g, st);
+    else launch_level<2>(A, D, level, g, st);
 }
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {

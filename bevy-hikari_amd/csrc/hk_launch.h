@@ -33,13 +33,16 @@ struct ViewArgs {
     float inverse_view_proj[16];
 };
 
+// All channels of one frame (post_process.rs:1199-1223 runs them one after another).
 struct DenoiseArgs {
-    const uint2* albedo;   // S
-    const uint2* render;   // s
-    const float* variance; // s
-    uint2* internal[4];
-    float* internal_variance;
-    uint2* output;
+    int channels;            // 3, or 2 when indirect_bounces == 0 (post_process.rs:949-954)
+    const uint2* albedo;     // S
+    const uint2* render[3];  // s
+    const float* variance[3];
+    uint2* internal[3][4];
+    float* internal_variance[3];
+    uint2* output[3];
+    float4* geom;            // 2 x float4 per pixel: (normal, depth), (instance, depth gradient)
 };
 
 struct ToneArgs {
@@ -55,7 +58,7 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st);
 void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st);
-void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, bool firefly, hipStream_t st);
+void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st);
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st);
 void launch_trace(const Scene& sc, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl,
                   uint32_t n, uint32_t* hits, unsigned long long* top, hipStream_t st);

@@ -66,8 +66,10 @@ struct hk_ctx {
     uint4* reservoirs[HK_RESERVOIR_BUFFERS] = {};
     uint32_t res_n = 0;
     // denoise
-    uint2* internal[4] = {};
-    float* internal_variance = nullptr;
+    uint2* internal[3][4] = {};
+    float* internal_variance[3] = {};
+    float4* geom = nullptr;
+    int last_denoised_channels = 3;
     uint2* denoised[3] = {};
     uint2* tone = nullptr;
     // counters (top, emitter, primary)
@@ -120,8 +122,11 @@ void free_targets(hk_ctx* c)
         release(c->denoised[i]);
     }
     for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) release(c->reservoirs[i]);
-    for (int i = 0; i < 4; ++i) release(c->internal[i]);
-    release(c->internal_variance);
+    for (int ch = 0; ch < 3; ++ch) {
+        for (int i = 0; i < 4; ++i) release(c->internal[ch][i]);
+        release(c->internal_variance[ch]);
+    }
+    release(c->geom);
     release(c->tone);
     c->sized = false;
 }
@@ -423,12 +428,16 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
         HK_HIP(c, hipMalloc(&c->reservoirs[i], 4 * sp * sizeof(uint4)));
         HK_HIP(c, hipMemset(c->reservoirs[i], 0, 4 * sp * sizeof(uint4)));  // light.rs:355-358 zero-fill
     }
-    for (int i = 0; i < 4; ++i) {
-        HK_HIP(c, hipMalloc(&c->internal[i], sp * sizeof(uint2)));
-        HK_HIP(c, hipMemset(c->internal[i], 0, sp * sizeof(uint2)));
+    for (int ch = 0; ch < 3; ++ch) {
+        for (int i = 0; i < 4; ++i) {
+            HK_HIP(c, hipMalloc(&c->internal[ch][i], sp * sizeof(uint2)));
+            HK_HIP(c, hipMemset(c->internal[ch][i], 0, sp * sizeof(uint2)));
+        }
+        HK_HIP(c, hipMalloc(&c->internal_variance[ch], sp * sizeof(float)));
+        HK_HIP(c, hipMemset(c->internal_variance[ch], 0, sp * sizeof(float)));
     }
-    HK_HIP(c, hipMalloc(&c->internal_variance, sp * sizeof(float)));
-    HK_HIP(c, hipMemset(c->internal_variance, 0, sp * sizeof(float)));
+    HK_HIP(c, hipMalloc(&c->geom, 2 * sp * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->geom, 0, 2 * sp * sizeof(float4)));
     HK_HIP(c, hipMalloc(&c->tone, sp * sizeof(uint2)));
     HK_HIP(c, hipMemset(c->tone, 0, sp * sizeof(uint2)));
     HK_HIP(c, hipDeviceSynchronize());
@@ -542,20 +551,21 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     hipStream_t st = pick(c, stream);
     FrameArgs A = frame_args(c, settings, in);
     int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
-    for (int ch = 0; ch < channels; ++ch) {
-        DenoiseArgs D;
-        D.albedo = c->albedo;
-        D.render = c->render[ch];
-        D.variance = c->variance[ch];
-        for (int i = 0; i < 4; ++i) D.internal[i] = c->internal[i];
-        D.internal_variance = c->internal_variance;
-        D.output = c->denoised[ch];
-        timed(c, "demodulation", st, [&] { launch_demod(A, D, st); });
-        for (int level = 0; level < 4; ++level) {
-            bool ff = ch >= 1;  // denoise_direct has no FIREFLY_FILTERING (post_process.rs:1193-1197)
-            timed(c, ff ? "denoise_firefly" : "denoise", st, [&] { launch_denoise(A, D, level, ff, st); });
-        }
+    DenoiseArgs D;
+    std::memset(&D, 0, sizeof(D));
+    D.channels = channels;
+    D.albedo = c->albedo;
+    for (int ch = 0; ch < 3; ++ch) {
+        D.render[ch] = c->render[ch];
+        D.variance[ch] = c->variance[ch];
+        for (int i = 0; i < 4; ++i) D.internal[ch][i] = c->internal[ch][i];
+        D.internal_variance[ch] = c->internal_variance[ch];
+        D.output[ch] = c->denoised[ch];
     }
+    D.geom = c->geom;
+    c->last_denoised_channels = channels;
+    timed(c, "demodulation", st, [&] { launch_demod(A, D, st); });
+    for (int level = 0; level < 4; ++level) timed(c, "denoise", st, [&] { launch_denoise(A, D, level, st); });
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -598,7 +608,7 @@ static void* output_ptr(hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* b
     case HK_OUT_GBUF_DEPTH_GRADIENT: p = c->g_depth_gradient; W = c->S[0]; H = (uint32_t)c->S_rows; B = 8; break;
     case HK_OUT_GBUF_INSTANCE_MATERIAL: p = c->g_instance_material; W = c->S[0]; H = (uint32_t)c->S_rows; B = 8; break;
     case HK_OUT_GBUF_VELOCITY_UV: p = c->g_velocity_uv; W = c->S[0]; H = (uint32_t)c->S_rows; B = 16; break;
-    case HK_OUT_DENOISE_INTERNAL_VARIANCE: p = c->internal_variance; B = 4; break;
+    case HK_OUT_DENOISE_INTERNAL_VARIANCE: p = c->internal_variance[c->last_denoised_channels - 1]; B = 4; break;
     default: return nullptr;
     }
     if (w) *w = W;
