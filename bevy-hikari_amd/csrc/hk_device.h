@@ -148,17 +148,55 @@ struct Counters {
     unsigned long long* primary;
 };
 
+// ------------------------------------------------------------------ f16 (hardware)
+// v_cvt_f16_f32 rounds to nearest-even with f16 denormals kept (default MODE), which is the
+// IEEE conversion hk_f32_to_f16 restates in software for the oracle; v_cvt_f32_f16 is exact.
+// Both directions are inline asm so the optimiser cannot fold them into neighbouring f32
+// arithmetic (f16 narrowing of fpext'd operands, v_fma_mix* selection): every value is rounded
+// to f32 first and then to f16, as the reference's f32 shader math + pack2x16float does.
+HKD uint32_t f16_bits(float f) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f); }
+HKD float f16_val(uint32_t h)
+{
+    float r;
+    asm("v_cvt_f32_f16 %0, %1" : "=v"(r) : "v"(h));
+    return r;
+}
+#ifdef HK_SOFT_F16
+#define f16_bits hk_f32_to_f16
+#define f16_val(h) hk_f16_to_f32((h) & 0xFFFFu)
+#endif
+#ifdef HK_SOFT_F16
+HKD uint32_t pack2x16float(float a, float b) { return f16_bits(a) | (f16_bits(b) << 16); }
+#else
+// asm as well: a plain fptrunc(fmul(a, b)) is selected as v_fma_mixlo_f16, which rounds the
+// exact product once to f16 instead of to f32 then f16 (the reference's two roundings).
+HKD uint32_t pack2x16float(float a, float b)
+{
+    uint32_t r;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+#endif
+HKD float unpack_lo16float(uint32_t v) { return f16_val(v); }
+HKD float unpack_hi16float(uint32_t v)
+{
+#ifdef HK_SOFT_F16
+    return f16_val(v >> 16);
+#endif
+    float r;
+    asm("v_cvt_f32_f16_sdwa %0, %1 src0_sel:WORD_1" : "=v"(r) : "v"(v));
+    return r;
+}
+
 // ------------------------------------------------------------------ texel access
 HKD void store_rgba16f(uint2* tex, int32_t idx, f4 c)
 {
-    uint32_t a = hk_f32_to_f16(c.x) | (hk_f32_to_f16(c.y) << 16);
-    uint32_t b = hk_f32_to_f16(c.z) | (hk_f32_to_f16(c.w) << 16);
-    tex[idx] = make_uint2(a, b);
+    tex[idx] = make_uint2(pack2x16float(c.x, c.y), pack2x16float(c.z, c.w));
 }
 HKD f4 load_rgba16f(const uint2* tex, int32_t idx)
 {
     uint2 v = tex[idx];
-    return mk4(hk_unpack_lo16float(v.x), hk_unpack_hi16float(v.x), hk_unpack_lo16float(v.y), hk_unpack_hi16float(v.y));
+    return mk4(unpack_lo16float(v.x), unpack_hi16float(v.x), unpack_lo16float(v.y), unpack_hi16float(v.y));
 }
 
 // Deferred-texture addressing: frame-OOB -> 0 (textureLoad robustness); in-frame rows outside
@@ -270,12 +308,12 @@ HKD Reservoir zero_reservoir()
 HKD Reservoir unpack_reservoir(uint4 c0, uint4 c1, uint4 c2, uint4 c3)
 {
     Reservoir r;
-    r.count = hk_unpack_lo16float(c3.z);
-    r.w = hk_unpack_hi16float(c3.z);
-    r.w_sum = hk_unpack_lo16float(c3.w);
-    r.w2_sum = hk_unpack_hi16float(c3.w);
-    r.s.radiance = mk4(hk_unpack_lo16float(c0.x), hk_unpack_hi16float(c0.x), hk_unpack_lo16float(c0.y),
-                       hk_unpack_hi16float(c0.y));
+    r.count = unpack_lo16float(c3.z);
+    r.w = unpack_hi16float(c3.z);
+    r.w_sum = unpack_lo16float(c3.w);
+    r.w2_sum = unpack_hi16float(c3.w);
+    r.s.radiance = mk4(unpack_lo16float(c0.x), unpack_hi16float(c0.x), unpack_lo16float(c0.y),
+                       unpack_hi16float(c0.y));
     r.s.random = mk4(hk_unpack_unorm16(c0.z), hk_unpack_unorm16(c0.z >> 16), hk_unpack_unorm16(c0.w),
                      hk_unpack_unorm16(c0.w >> 16));
     r.s.visible_position = mk4(__uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z), __uint_as_float(c1.w));
@@ -296,10 +334,10 @@ HKD Reservoir load_res(const ResBuf& b, int32_t i)
 HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
 {
     uint4 c0, c1, c2, c3;
-    c3.z = hk_pack2x16float(r.count, r.w);
-    c3.w = hk_pack2x16float(r.w_sum, r.w2_sum);
-    c0.x = hk_pack2x16float(r.s.radiance.x, r.s.radiance.y);
-    c0.y = hk_pack2x16float(r.s.radiance.z, r.s.radiance.w);
+    c3.z = pack2x16float(r.count, r.w);
+    c3.w = pack2x16float(r.w_sum, r.w2_sum);
+    c0.x = pack2x16float(r.s.radiance.x, r.s.radiance.y);
+    c0.y = pack2x16float(r.s.radiance.z, r.s.radiance.w);
     c0.z = hk_pack2x16unorm(r.s.random.x, r.s.random.y);
     c0.w = hk_pack2x16unorm(r.s.random.z, r.s.random.w);
     c1 = make_uint4(__float_as_uint(r.s.visible_position.x), __float_as_uint(r.s.visible_position.y),

@@ -18,16 +18,39 @@
 
 namespace hk {
 
-// workgroup tile -> pixel (global coordinates)
+// workgroup tile -> pixel (global coordinates).
+// Traversal kernels keep the raster tile order: workgroups are dealt round-robin over the 8
+// XCDs, so every XCD works on the same band of the frame at once and per-region cost differences
+// (sky vs. geometry, lit vs. shadowed) are spread evenly (an XCD-stripe order measured 20% slower
+// on cornell 1080p: the XCD holding the expensive stripe finishes last).
+// Neighbour-gather kernels (a-trous levels, demodulation) have uniform cost and use the
+// XCD-stripe order (cdna_hip_programming.md T1, bijective form): workgroup L runs on XCD L % 8,
+// and each XCD gets a contiguous range of tiles in raster order, so the taps hit its own L2.
+template <bool XCD_STRIPES = false>
 HKD bool tile_pixel(uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
 {
+    const uint32_t gx = gridDim.x;
+    const uint32_t L = blockIdx.x + blockIdx.y * gx;
+    uint32_t tile = L;
+    if (XCD_STRIPES) {
+        const uint32_t n = gridDim.x * gridDim.y;
+        const uint32_t xcd = L & 7u, i = L >> 3, q = n >> 3, r = n & 7u;
+        tile = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + i;
+    }
+    const uint32_t tx = tile % gx, ty = tile / gx;
     uint32_t t = threadIdx.x;
     uint32_t w = t >> 6, lane = t & 63u;
-    x = (int32_t)(blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u));
-    int32_t ly = (int32_t)(blockIdx.y * 16u + (w >> 1) * 8u + (lane >> 3));
+    x = (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
+    int32_t ly = (int32_t)(ty * 16u + (w >> 1) * 8u + (lane >> 3));
     y = row0 + ly;
     return (uint32_t)x < width && ly < rows;
 }
+
+#ifdef HK_SPATIAL_STRIPES
+constexpr bool SPATIAL_STRIPES = true;
+#else
+constexpr bool SPATIAL_STRIPES = false;
+#endif
 
 // ------------------------------------------------------------------ G-buffer
 HKD f3 primary_direction(const ViewArgs& V, float px, float py, const uint32_t* size)
@@ -530,7 +553,7 @@ template <bool EMISSIVE_LIT>
 __global__ __launch_bounds__(256) void k_spatial(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
-    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y);
+    if (tile_pixel<SPATIAL_STRIPES>(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y);
 }
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
@@ -564,7 +587,7 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<true>(F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     f2 uv = coords_to_uv(x, y, F.s);
     f2 duv = jittered_uv(F, uv, 0.5f);
@@ -603,7 +626,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<true>(F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     constexpr int32_t step = 8 >> LEVEL;
     const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
@@ -689,7 +712,7 @@ __global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<true>(F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     f4 c = load_rgba16f(T.direct, idx);
     f4 e = load_rgba16f(T.emissive, idx);
@@ -785,6 +808,17 @@ void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {
     hipLaunchKernelGGL(k_tone, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
 }
+__global__ __launch_bounds__(256) void k_f16(const float* in, uint32_t n, uint16_t* out)
+{
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) out[i] = (uint16_t)(pack2x16float(in[i], 0.0f) & 0xFFFFu);
+}
+
+void launch_f16(const float* in, uint32_t n, uint16_t* out, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_f16, dim3((n + 255u) / 256u), dim3(256), 0, st, in, n, out);
+}
+
 void launch_trace(const Scene& sc, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl,
                   uint32_t n, uint32_t* hits, unsigned long long* top, hipStream_t st)
 {

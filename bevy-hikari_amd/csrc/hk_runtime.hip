@@ -787,4 +787,24 @@ int hk_trace(hk_ctx* c, const float* rays, const float* max_d, const float* earl
     return HK_OK;
 }
 
+int hk_selftest_f16(hk_ctx* c, const float* in, uint32_t n, uint16_t* out)
+{
+    if (!c || (n && (!in || !out))) return HK_ERR_INVALID;
+    if (n == 0) return HK_OK;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, nullptr);
+    float* d_in = nullptr;
+    uint16_t* d_out = nullptr;
+    HK_HIP(c, hipMalloc(&d_in, (size_t)n * 4));
+    HK_HIP(c, hipMalloc(&d_out, (size_t)n * 2));
+    HK_HIP(c, hipMemcpy(d_in, in, (size_t)n * 4, hipMemcpyHostToDevice));
+    launch_f16(d_in, n, d_out, st);
+    HK_HIP(c, hipGetLastError());
+    HK_HIP(c, hipMemcpyAsync(out, d_out, (size_t)n * 2, hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    release(d_in);
+    release(d_out);
+    return HK_OK;
+}
+
 }  // extern "C"

@@ -150,6 +150,13 @@ class HikariRenderer:
                                           None), "hk_trace")
         return hits
 
+    def selftest_f16(self, values: np.ndarray) -> np.ndarray:
+        """The kernels' own f32 -> f16 conversion applied to `values` (uint16 bit patterns)."""
+        v = np.ascontiguousarray(values, np.float32)
+        out = np.empty(len(v), np.uint16)
+        _check(self.ctx, self._L.hk_selftest_f16(self.ctx, v.ctypes.data, len(v), out.ctypes.data), "hk_selftest_f16")
+        return out
+
 
 class HikariPlugin:
     """`app.add_plugin(HikariPlugin)` for one camera: owns the renderer and the frame counter

@@ -217,6 +217,10 @@ int hk_kernel_timing(hk_ctx* ctx, const char** names, float* ms, int capacity);
 int hk_trace(hk_ctx* ctx, const float* rays, const float* max_distance, const float* early_distance,
              const uint32_t* exclude_instance, uint32_t n, void* hits, int device_ptrs, void* stream);
 
+/* ---- self-test of the device f16 conversion (pack2x16float, light.wgsl:173-216 pack_reservoir)
+ * converts n host floats with the kernels' own conversion; out: n f16 bit patterns (host) */
+int hk_selftest_f16(hk_ctx* ctx, const float* in, uint32_t n, uint16_t* out);
+
 #ifdef __cplusplus
 }
 #endif

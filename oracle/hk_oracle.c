@@ -1934,4 +1934,9 @@ float hko_log2(float x) { return hk_log2(x); }
 float hko_sin(float x) { return hk_sin(x); }
 float hko_cos(float x) { return hk_cos(x); }
 uint32_t hko_f32_to_f16(float x) { return hk_f32_to_f16(x); }
+void hko_f32_to_f16_array(const float* in, size_t n, uint16_t* out)
+{
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)n; ++i) out[i] = (uint16_t)hk_f32_to_f16(in[i]);
+}
 uint32_t hko_hash(uint32_t x) { return hk_hash(x); }

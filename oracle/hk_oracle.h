@@ -61,6 +61,7 @@ float hko_log2(float x);
 float hko_sin(float x);
 float hko_cos(float x);
 uint32_t hko_f32_to_f16(float x);
+void hko_f32_to_f16_array(const float* in, size_t n, uint16_t* out);
 uint32_t hko_hash(uint32_t x);
 
 #ifdef __cplusplus

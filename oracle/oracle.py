@@ -52,6 +52,7 @@ def lib() -> C.CDLL:
         "hko_sin": (f, [f]),
         "hko_cos": (f, [f]),
         "hko_f32_to_f16": (u32, [f]),
+        "hko_f32_to_f16_array": (None, [C.c_void_p, C.c_size_t, C.c_void_p]),
         "hko_hash": (u32, [u32]),
     }
     for name, (res, args) in sigs.items():

@@ -384,3 +384,19 @@ def test_denoiser_matches_numpy_restatement():
     got = h16(o.output(7))[..., :3]
     rel = np.abs(got - irr) / np.maximum(np.abs(irr), 1e-2)
     assert np.mean(rel.max(axis=-1) < 1e-2) >= 0.99, float(np.mean(rel.max(axis=-1) < 1e-2))
+
+
+def test_f16_conversion_matches_numpy_ieee_sweep():
+    """hk_f32_to_f16 (software RNE, shared by the oracle) equals IEEE-754 binaryfloat16 conversion
+    (numpy's astype) on a 2^24-pattern stride sweep of all f32 bit patterns (NaNs: quiet NaN)."""
+    import oracle as orc
+    L = orc.lib()
+    bits = np.arange(0, 1 << 32, 256, dtype=np.uint64).astype(np.uint32) + np.uint32(0x1000 - 3)
+    vals = bits.view(np.float32)
+    got = np.empty(len(vals), np.uint16)
+    L.hko_f32_to_f16_array(vals.ctypes.data, len(vals), got.ctypes.data)
+    with np.errstate(over="ignore"):
+        want = vals.astype(np.float16).view(np.uint16)
+    nan = np.isnan(vals)
+    assert np.array_equal(got[~nan], want[~nan])
+    assert ((got[nan] & 0x7C00) == 0x7C00).all() and ((got[nan] & 0x3FF) != 0).all()
