@@ -106,15 +106,16 @@ def cpu_baseline(scene_desc, cam, lights, st, w, h, budget_s: float) -> dict:
                       f"(C restatement of light.wgsl/denoise.wgsl, {threads} OpenMP threads)"}
 
 
-def load_pmc_traffic(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), if present."""
+def load_pmc_traffic(config: str, kernel: str):
+    """HBM bytes per launch of `kernel` under `config` from the committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py), if present."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
-        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
+        return d["configs"][config]["kernels"][kernel].get("hbm_bytes_per_launch")
+    except (KeyError, ValueError):
         return None
 
 
@@ -213,7 +214,7 @@ def main():
         pix = W * rows
         alg = BYTES_PER_PIXEL.get(dom, 0) * pix
         achieved = alg / (timing[dom] * 1e-3) / 1e9
-        traffic = load_pmc_traffic(dom)
+        traffic = load_pmc_traffic(args.config, dom)
         result = {
             "metric": "Mrays/sec + ms/frame @1080p 1spp; cornell & city scenes, 1/2/4/8 GPU",
             "value": round(mrays, 2),

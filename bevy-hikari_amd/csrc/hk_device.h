@@ -509,13 +509,14 @@ HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t nod
         f3 mn, mx;
         uint32_t entry, exit;
         load_node(sc.asset_nodes, node_offset + index, mn, entry, mx, exit);
+        // leaves carry their triangle's box (k_fill_blas_leaves): the same slab test as
+        // light.wgsl:411-413 on the recomputed box, before the triangle is fetched
+        const bool pass = intersects_aabb(ray, mn, mx) < hit.distance;
         if (entry >= HK_BVH_LEAF_FLAG) {
-            uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
-            f3 a, b, c;
-            load_triangle(sc.primitives, primitive_index, a, b, c);
-            f3 tmn = vmin(a, vmin(b, c));
-            f3 tmx = vmax(a, vmax(b, c));
-            if (intersects_aabb(ray, tmn, tmx) < hit.distance) {
+            if (pass) {
+                uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
+                f3 a, b, c;
+                load_triangle(sc.primitives, primitive_index, a, b, c);
                 f2 uv;
                 float d = intersects_triangle(ray, a, b, c, uv);
                 if (d < hit.distance) {
@@ -528,7 +529,7 @@ HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t nod
             }
             index = exit;
         } else {
-            index = intersects_aabb(ray, mn, mx) < hit.distance ? entry : exit;
+            index = pass ? entry : exit;
         }
     }
     return intersected;
@@ -541,6 +542,7 @@ HKD f3 world_to_local_point(const hk_instance& in, f3 p)
     float y = ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7] * 1.0f;
     float z = ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11] * 1.0f;
     float w = ((m[12] * p.x + m[13] * p.y) + m[14] * p.z) + m[15] * 1.0f;
+    if (w == 1.0f) return mk3(x, y, z);  // x / 1 == x exactly: skips three IEEE divides (affine transforms)
     return mk3(x / w, y / w, z / w);
 }
 HKD f3 world_to_local_dir(const hk_instance& in, f3 p)
@@ -554,6 +556,7 @@ HKD f3 world_to_local_dir(const hk_instance& in, f3 p)
 HKD f3 local_to_world_point(const hk_instance& in, f3 p)
 {
     f4 r = mat4_mul(in.model, mk4(p.x, p.y, p.z, 1.0f));
+    if (r.w == 1.0f) return mk3(r.x, r.y, r.z);  // exact, as in world_to_local_point
     return mk3(r.x / r.w, r.y / r.w, r.z / r.w);
 }
 HKD f3 local_to_world_normal(const hk_instance& in, f3 n)
@@ -582,7 +585,8 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
         if (entry >= HK_BVH_LEAF_FLAG) {
             uint32_t instance_index = entry - HK_BVH_LEAF_FLAG;
             const hk_instance& in = sc.instances[instance_index];
-            if (instance_index != exclude && intersects_aabb(ray, ld3(in.min), ld3(in.max)) < hit.distance) {
+            // leaf box = the instance's min/max (k_fill_tlas_leaves), light.wgsl:456-457
+            if (instance_index != exclude && intersects_aabb(ray, mn, mx) < hit.distance) {
                 Ray r;
                 r.origin = world_to_local_point(in, ray.origin);
                 r.direction = world_to_local_dir(in, ray.direction);

@@ -23,7 +23,9 @@ namespace hk {
 // XCDs, so every XCD works on the same band of the frame at once and per-region cost differences
 // (sky vs. geometry, lit vs. shadowed) are spread evenly (an XCD-stripe order measured 20% slower
 // on cornell 1080p: the XCD holding the expensive stripe finishes last).
-// Neighbour-gather kernels (a-trous levels, demodulation) have uniform cost and use the
+// Spatial reuse measured the same either way and keeps the raster order (its depth window
+// origin is the raster tile). Neighbour-gather kernels (a-trous levels, demodulation) have
+// uniform cost and use the
 // XCD-stripe order (cdna_hip_programming.md T1, bijective form): workgroup L runs on XCD L % 8,
 // and each XCD gets a contiguous range of tiles in raster order, so the taps hit its own L2.
 template <bool XCD_STRIPES = false>
@@ -46,11 +48,22 @@ HKD bool tile_pixel(uint32_t width, int32_t row0, int32_t rows, int32_t& x, int3
     return (uint32_t)x < width && ly < rows;
 }
 
-#ifdef HK_SPATIAL_STRIPES
-constexpr bool SPATIAL_STRIPES = true;
-#else
-constexpr bool SPATIAL_STRIPES = false;
+// Occupancy hints for the traversal kernels (waves per SIMD); tunable at build time.
+#ifndef HK_TRACE_WAVES
+#define HK_TRACE_WAVES 0
 #endif
+#if HK_TRACE_WAVES > 0
+#define HK_TRACE_OCC __attribute__((amdgpu_waves_per_eu(HK_TRACE_WAVES, 8)))
+#else
+#define HK_TRACE_OCC
+#endif
+
+// origin (global coordinates) of this workgroup's tile in the raster order
+HKD void tile_origin(int32_t row0, int32_t& x0, int32_t& y0)
+{
+    x0 = (int32_t)(blockIdx.x * 16u);
+    y0 = row0 + (int32_t)(blockIdx.y * 16u);
+}
 
 // ------------------------------------------------------------------ G-buffer
 HKD f3 primary_direction(const ViewArgs& V, float px, float py, const uint32_t* size)
@@ -67,7 +80,7 @@ HKD float ndc_depth(const float* vp, f3 p)
     return c.z / c.w;
 }
 
-__global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V)
+__global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewArgs V)
 {
     int32_t x, y;
     bool active = tile_pixel(A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
@@ -260,7 +273,7 @@ HKD void direct_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_
 }
 
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE>
-__global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) HK_TRACE_OCC void k_direct(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
@@ -431,7 +444,7 @@ HKD void indirect_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int3
 }
 
 template <bool MULTI>
-__global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) HK_TRACE_OCC void k_indirect(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
@@ -445,8 +458,27 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
 // The reference's workgroup-shared copies (shared_reservoir/shared_depth) hold exactly the
 // values the global path reads for in-tile neighbours, so every neighbour is read from the
 // (L2-resident) reservoir planes directly.
+// Depth window of spatial reuse: at upscale ratio 1 every neighbour and screen-space occlusion
+// tap of a 16x16 tile lies within RANGE (20) + 2 pixels of it, so the workgroup stages that
+// 60x60 window of G-buffer depth in LDS once (14 KiB) instead of ~80 scattered 16-byte position
+// loads per pixel.  Values are load_depth() of the same coordinates (frame-OOB -> 0, band
+// clamp), so results are unchanged; a coordinate outside the window reads global memory.
+constexpr int32_t SP_HALO = 22, SP_WIN = 16 + 2 * SP_HALO;
+struct DepthWin {
+    const float* lds;  // null: no window (upscale ratio != 1)
+    int32_t x0, y0;
+};
+HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t x, int32_t y)
+{
+    if (W.lds) {
+        uint32_t lx = (uint32_t)(x - W.x0), ly = (uint32_t)(y - W.y0);
+        if (lx < (uint32_t)SP_WIN && ly < (uint32_t)SP_WIN) return W.lds[ly * SP_WIN + lx];
+    }
+    return load_depth(F, G, x, y);
+}
+
 template <bool EMISSIVE_LIT>
-HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y)
+HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y, const DepthWin& W)
 {
     const Frame& F = A.F;
     constexpr uint32_t COUNT = EMISSIVE_LIT ? 8u : 16u;
@@ -498,7 +530,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         if (suv.x < 0.0f || suv.y < 0.0f || suv.x > 1.0f || suv.y > 1.0f) continue;
         int32_t sdx, sdy;
         jittered_coords(F, suv, sdx, sdy);
-        float sample_depth = load_depth(F, A.G, sdx, sdy);
+        float sample_depth = win_depth(F, A.G, W, sdx, sdy);
         float depth_ratio = depth / sample_depth;
         if (depth_ratio < 0.9f || depth_ratio > 1.1f) continue;
         q = load_res(C.cur, s_index(F, scx, scy));
@@ -517,7 +549,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             f2 tuv = mk2(uv.x + (tap_dist * dir.x) / (float)F.s[0], uv.y + (tap_dist * dir.y) / (float)F.s[1]);
             int32_t tdx, tdy;
             jittered_coords(F, tuv, tdx, tdy);
-            float tap_depth = load_depth(F, A.G, tdx, tdy);
+            float tap_depth = win_depth(F, A.G, W, tdx, tdy);
             float ref_depth = hk_mixf(depth, sample_depth, (float)j / (float)(tap_count + 1u));
             if (tap_depth > ref_depth + 0.00001f) {
                 occluded = true;
@@ -549,11 +581,23 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     store_rgba16f(C.render, idx, mk4(oc.x, oc.y, oc.z, 1.0f));
 }
 
-template <bool EMISSIVE_LIT>
-__global__ __launch_bounds__(256) void k_spatial(FrameArgs A, ChannelArgs C)
+template <bool EMISSIVE_LIT, bool WINDOW>
+__global__ __launch_bounds__(256) HK_TRACE_OCC void k_spatial(FrameArgs A, ChannelArgs C)
 {
+    __shared__ float win[WINDOW ? SP_WIN * SP_WIN : 1];
+    DepthWin W{nullptr, 0, 0};
+    if (WINDOW) {
+        int32_t x0, y0;
+        tile_origin(A.F.s_row0, x0, y0);
+        W.x0 = x0 - SP_HALO;
+        W.y0 = y0 - SP_HALO;
+        for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256)
+            win[k] = load_depth(A.F, A.G, W.x0 + k % SP_WIN, W.y0 + k / SP_WIN);
+        __syncthreads();
+        W.lds = win;
+    }
     int32_t x, y;
-    if (tile_pixel<SPATIAL_STRIPES>(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y);
+    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y, W);
 }
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
@@ -779,8 +823,15 @@ void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipSt
 void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
 {
     dim3 g = tiles(A.F.s[0], A.F.s_rows);
-    if (emissive_lit) hipLaunchKernelGGL(k_spatial<true>, g, dim3(256), 0, st, A, C);
-    else hipLaunchKernelGGL(k_spatial<false>, g, dim3(256), 0, st, A, C);
+    // the window assumes integrator pixels == deferred pixels (upscale ratio 1)
+    const bool window = A.F.upscale_ratio == 1.0f && A.F.s[0] == A.F.S[0] && A.F.s[1] == A.F.S[1];
+    if (emissive_lit) {
+        if (window) hipLaunchKernelGGL((k_spatial<true, true>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial<true, false>), g, dim3(256), 0, st, A, C);
+    } else {
+        if (window) hipLaunchKernelGGL((k_spatial<false, true>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial<false, false>), g, dim3(256), 0, st, A, C);
+    }
 }
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
 {
@@ -808,6 +859,44 @@ void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {
     hipLaunchKernelGGL(k_tone, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
 }
+// ------------------------------------------------------------------ scene preparation
+// The reference's flattened leaves carry an empty AABB and the kernels recompute the box of the
+// leaf's triangle / instance before testing it (light.wgsl:411-412, 456-457).  At upload the
+// device copy of each leaf gets exactly that box (same vmin/vmax expression on the device, or
+// the instance record's min/max), so the traversal reads it with the node and only fetches the
+// 48-byte triangle / 176-byte instance once the box test has passed.  Same tests, same order.
+__global__ __launch_bounds__(256) void k_fill_blas_leaves(hk_node* nodes, uint32_t n, const uint32_t* prim_offset,
+                                                          const hk_primitive* prims)
+{
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || prim_offset[i] == HK_U32_MAX) return;
+    hk_node& nd = nodes[i];
+    if (nd.entry_index < HK_BVH_LEAF_FLAG) return;
+    f3 a, b, c;
+    load_triangle(prims, prim_offset[i] + nd.entry_index - HK_BVH_LEAF_FLAG, a, b, c);
+    f3 mn = vmin(a, vmin(b, c)), mx = vmax(a, vmax(b, c));
+    nd.min[0] = mn.x, nd.min[1] = mn.y, nd.min[2] = mn.z;
+    nd.max[0] = mx.x, nd.max[1] = mx.y, nd.max[2] = mx.z;
+}
+__global__ __launch_bounds__(256) void k_fill_tlas_leaves(hk_node* nodes, uint32_t n, const hk_instance* inst,
+                                                          uint32_t n_inst)
+{
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    hk_node& nd = nodes[i];
+    if (nd.entry_index < HK_BVH_LEAF_FLAG || nd.entry_index - HK_BVH_LEAF_FLAG >= n_inst) return;
+    const hk_instance& in = inst[nd.entry_index - HK_BVH_LEAF_FLAG];
+    for (int k = 0; k < 3; ++k) nd.min[k] = in.min[k], nd.max[k] = in.max[k];
+}
+void launch_fill_leaves(hk_node* blas, uint32_t n_blas, const uint32_t* prim_offset, const hk_primitive* prims,
+                        hk_node* tlas, uint32_t n_tlas, const hk_instance* inst, uint32_t n_inst, hipStream_t st)
+{
+    if (n_blas) hipLaunchKernelGGL(k_fill_blas_leaves, dim3((n_blas + 255u) / 256u), dim3(256), 0, st, blas, n_blas,
+                                   prim_offset, prims);
+    if (n_tlas) hipLaunchKernelGGL(k_fill_tlas_leaves, dim3((n_tlas + 255u) / 256u), dim3(256), 0, st, tlas, n_tlas,
+                                   inst, n_inst);
+}
+
 __global__ __launch_bounds__(256) void k_f16(const float* in, uint32_t n, uint16_t* out)
 {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;

@@ -350,6 +350,26 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
         if (arr[i]->count) HK_HIP(c, hipMemcpy(c->buf[i], arr[i]->data, arr[i]->count * elem[i], hipMemcpyHostToDevice));
         c->count[i] = arr[i]->count;
     }
+    // leaf boxes of the device node copies (see k_fill_blas_leaves): BLAS node -> primitive
+    // offset of the mesh that owns it, from the instances' mesh indices
+    const uint32_t n_blas = d->asset_nodes.count;
+    if (n_blas) {
+        std::vector<uint32_t> prim_offset(n_blas, HK_U32_MAX);
+        const hk_instance* inst = (const hk_instance*)d->instances.data;
+        for (uint32_t k = 0; k < d->instances.count; ++k) {
+            const hk_mesh_index& m = inst[k].mesh;
+            for (uint32_t j = 0; j < m.node[1]; ++j)
+                if ((size_t)m.node[0] + j < n_blas) prim_offset[m.node[0] + j] = m.primitive;
+        }
+        uint32_t* d_off = nullptr;
+        HK_HIP(c, hipMalloc(&d_off, (size_t)n_blas * 4));
+        HK_HIP(c, hipMemcpy(d_off, prim_offset.data(), (size_t)n_blas * 4, hipMemcpyHostToDevice));
+        launch_fill_leaves((hk_node*)c->buf[2], n_blas, d_off, (const hk_primitive*)c->buf[1], (hk_node*)c->buf[5],
+                           c->count[5], (const hk_instance*)c->buf[4], c->count[4], c->stream);
+        HK_HIP(c, hipGetLastError());
+        HK_HIP(c, hipStreamSynchronize(c->stream));
+        release(d_off);
+    }
     c->has_scene = true;
     return HK_OK;
 }
