@@ -101,6 +101,9 @@ struct Scene {
     const hk_node* emissive_nodes;
     const hk_emissive* emissives;
     uint32_t n_instances, n_instance_nodes, n_materials, n_emissive_nodes;
+    // G-buffer traversal layout (k_build_wide): per subtree start, both child boxes + starts
+    const float4* blas_wide;
+    const float4* tlas_wide;
 };
 
 // Frame-uniform + view + lights constants (view.rs:105-123, mesh_view_bindings.wgsl).
@@ -602,6 +605,123 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
         }
     }
     return hit;
+}
+
+// ------------------------------------------------------------------ G-buffer visibility
+// Ordered closest-hit traversal, the build's own primary-visibility rule (the reference
+// rasterises the G-buffer); defined in oracle/hk_oracle.c (closest_hit_ordered) and reproduced
+// here step for step.  Wide entry of a subtree start p (4 x float4, one 64-byte line):
+//   inner: (left box min, left subtree start), (left box max, right subtree start),
+//          (right box min, -), (right box max, -)      [starts mesh-local for BLAS]
+//   leaf:  (leaf box min, entry = payload | LEAF), (leaf box max, -)
+// Leaf boxes are the triangle's / instance's box, as the reference walk tests them.
+constexpr int GB_STACK = 64;
+struct GbStack {
+    uint32_t node[GB_STACK];
+    float t[GB_STACK];
+    int sp;
+};
+HKD bool gb_pop(GbStack& s, int base, float best, uint32_t& n)
+{
+    while (s.sp > base) {
+        s.sp--;
+        if (s.t[s.sp] < best) {
+            n = s.node[s.sp];
+            return true;
+        }
+    }
+    return false;
+}
+// one inner step: enter the nearer passing child, push the farther; false if neither passes
+HKD bool gb_descend(GbStack& s, const Ray& ray, float4 a, float4 b, float4 c, float4 d, float best, uint32_t& p)
+{
+    const float tl = intersects_aabb(ray, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
+    const float tr = intersects_aabb(ray, mk3(c.x, c.y, c.z), mk3(d.x, d.y, d.z));
+    const uint32_t ls = __float_as_uint(a.w), rs = __float_as_uint(b.w);
+    const bool hl = tl < best, hr = tr < best;
+    if (hl && hr) {
+        const bool right_first = tr < tl;
+        s.node[s.sp] = right_first ? ls : rs;
+        s.t[s.sp] = right_first ? tl : tr;
+        s.sp++;
+        p = right_first ? rs : ls;
+        return true;
+    }
+    if (hl) {
+        p = ls;
+        return true;
+    }
+    if (hr) {
+        p = rs;
+        return true;
+    }
+    return false;
+}
+HKD void closest_bottom_ordered(const Scene& sc, GbStack& s, Hit& hit, const Ray& ray, const hk_instance& in,
+                                uint32_t instance_index)
+{
+    const int sbase = s.sp;
+    const uint32_t base = in.mesh.node[0];
+    if (in.mesh.node[1] == 0u) return;
+    uint32_t p = 0u;  // mesh-local subtree start
+    for (;;) {
+        const float4* w = sc.blas_wide + 4u * (size_t)(base + p);
+        const float4 a = w[0], b = w[1];
+        const uint32_t entry = __float_as_uint(a.w);
+        bool go = false;
+        if (entry >= HK_BVH_LEAF_FLAG) {
+            if (intersects_aabb(ray, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance) {
+                const uint32_t primitive_index = in.mesh.primitive + entry - HK_BVH_LEAF_FLAG;
+                f3 t0, t1, t2;
+                load_triangle(sc.primitives, primitive_index, t0, t1, t2);
+                f2 uv;
+                const float dd = intersects_triangle(ray, t0, t1, t2, uv);
+                if (dd < hit.distance) {
+                    hit.distance = dd;
+                    hit.uv = uv;
+                    hit.primitive_index = primitive_index;
+                    hit.instance_index = instance_index;
+                }
+            }
+        } else {
+            go = gb_descend(s, ray, a, b, w[2], w[3], hit.distance, p);
+        }
+        if (go) continue;
+        if (!gb_pop(s, sbase, hit.distance, p)) return;
+    }
+}
+HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray)
+{
+    Hit hit;
+    hit.uv = mk2(0.0f, 0.0f);
+    hit.distance = HK_F32_MAX;
+    hit.instance_index = HK_U32_MAX;
+    hit.primitive_index = HK_U32_MAX;
+    if (sc.n_instance_nodes == 0u) return hit;
+    GbStack s;
+    s.sp = 0;
+    uint32_t p = 0u;
+    for (;;) {
+        const float4* w = sc.tlas_wide + 4u * (size_t)p;
+        const float4 a = w[0], b = w[1];
+        const uint32_t entry = __float_as_uint(a.w);
+        bool go = false;
+        if (entry >= HK_BVH_LEAF_FLAG) {
+            if (intersects_aabb(ray, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance) {
+                const uint32_t instance_index = entry - HK_BVH_LEAF_FLAG;
+                const hk_instance& in = sc.instances[instance_index];
+                Ray r;
+                r.origin = world_to_local_point(in, ray.origin);
+                r.direction = world_to_local_dir(in, ray.direction);
+                r.inv_direction = inv(r.direction);
+                closest_bottom_ordered(sc, s, hit, r, in, instance_index);
+            }
+        } else {
+            go = gb_descend(s, ray, a, b, w[2], w[3], hit.distance, p);
+        }
+        if (go) continue;
+        if (!gb_pop(s, 0, hit.distance, p)) return hit;
+    }
 }
 
 HKD const hk_instance& get_instance(const Scene& sc, uint32_t i) { return sc.instances[i < sc.n_instances ? i : sc.n_instances - 1]; }

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
         ray.origin = ld3(V.world_position);
         ray.direction = primary_direction(V, (float)x + 0.5f, (float)y + 0.5f, A.F.S);
         ray.inv_direction = inv(ray.direction);
-        Hit hit = traverse_top(A.sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+        Hit hit = closest_hit_ordered(A.sc, ray);
         if (hit.instance_index == HK_U32_MAX) {
             A.G.position[idx] = make_float4(0, 0, 0, 0);
             A.G.normal[idx] = 0u;
@@ -888,6 +888,37 @@ __global__ __launch_bounds__(256) void k_fill_tlas_leaves(hk_node* nodes, uint32
     const hk_instance& in = inst[nd.entry_index - HK_BVH_LEAF_FLAG];
     for (int k = 0; k < 3; ++k) nd.min[k] = in.min[k], nd.max[k] = in.max[k];
 }
+// Wide entries for the G-buffer traversal (hk_device.h closest_hit_ordered), built from the
+// prepared flat nodes: node_base/node_count = the owning mesh's node range (TLAS: 0, n).
+__global__ __launch_bounds__(256) void k_build_wide(const hk_node* flat, uint32_t n, const uint32_t* node_base,
+                                                    const uint32_t* node_count, float4* wide)
+{
+    uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n) return;
+    float4* w = wide + 4u * (size_t)p;
+    const hk_node& f = flat[p];
+    const uint32_t base = node_base ? node_base[p] : 0u, count = node_count ? node_count[p] : n;
+    w[0] = make_float4(f.min[0], f.min[1], f.min[2], __uint_as_float(f.entry_index));
+    w[1] = make_float4(f.max[0], f.max[1], f.max[2], 0.0f);
+    w[2] = make_float4(0, 0, 0, 0);
+    w[3] = make_float4(0, 0, 0, 0);
+    if (f.entry_index >= HK_BVH_LEAF_FLAG || base == HK_U32_MAX) return;
+    // inner subtree starting at p: left box node p (subtree p+1), right box node q (subtree q+1)
+    const uint32_t local = p - base, q_local = f.exit_index;
+    if (q_local >= count) return;  // p is a right-child box node, never a subtree start
+    const hk_node& g = flat[base + q_local];
+    w[0].w = __uint_as_float(local + 1u);
+    w[1].w = __uint_as_float(q_local + 1u);
+    w[2] = make_float4(g.min[0], g.min[1], g.min[2], 0.0f);
+    w[3] = make_float4(g.max[0], g.max[1], g.max[2], 0.0f);
+}
+void launch_build_wide(const hk_node* flat, uint32_t n, const uint32_t* node_base, const uint32_t* node_count,
+                       float4* wide, hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(k_build_wide, dim3((n + 255u) / 256u), dim3(256), 0, st, flat, n, node_base, node_count,
+                              wide);
+}
+
 void launch_fill_leaves(hk_node* blas, uint32_t n_blas, const uint32_t* prim_offset, const hk_primitive* prims,
                         hk_node* tlas, uint32_t n_tlas, const hk_instance* inst, uint32_t n_inst, hipStream_t st)
 {

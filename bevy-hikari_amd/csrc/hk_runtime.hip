@@ -41,6 +41,9 @@ struct hk_ctx {
     // scene
     void* buf[9] = {};
     uint32_t count[9] = {};
+    float4* blas_wide = nullptr;  // G-buffer traversal layout (k_build_wide)
+    float4* tlas_wide = nullptr;
+    uint32_t gb_stack_need = 0;   // TLAS + BLAS subtree depth bound of closest_hit_ordered
     bool has_scene = false;
     uchar4* noise = nullptr;
     bool has_noise = false;
@@ -197,6 +200,8 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.sc.n_instance_nodes = c->count[5];
     A.sc.n_materials = c->count[6];
     A.sc.n_emissive_nodes = c->count[7];
+    A.sc.blas_wide = c->blas_wide;
+    A.sc.tlas_wide = c->tlas_wide;
     Frame& F = A.F;
     hk_settings def;
     hk_settings_default(&def);
@@ -315,6 +320,8 @@ void hk_destroy(hk_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_targets(c);
     for (int i = 0; i < 9; ++i) release(c->buf[i]);
+    release(c->blas_wide);
+    release(c->tlas_wide);
     release(c->noise);
     release(c->counters);
     for (auto& t : c->pending) {
@@ -350,26 +357,63 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
         if (arr[i]->count) HK_HIP(c, hipMemcpy(c->buf[i], arr[i]->data, arr[i]->count * elem[i], hipMemcpyHostToDevice));
         c->count[i] = arr[i]->count;
     }
-    // leaf boxes of the device node copies (see k_fill_blas_leaves): BLAS node -> primitive
-    // offset of the mesh that owns it, from the instances' mesh indices
-    const uint32_t n_blas = d->asset_nodes.count;
-    if (n_blas) {
-        std::vector<uint32_t> prim_offset(n_blas, HK_U32_MAX);
-        const hk_instance* inst = (const hk_instance*)d->instances.data;
-        for (uint32_t k = 0; k < d->instances.count; ++k) {
-            const hk_mesh_index& m = inst[k].mesh;
-            for (uint32_t j = 0; j < m.node[1]; ++j)
-                if ((size_t)m.node[0] + j < n_blas) prim_offset[m.node[0] + j] = m.primitive;
+    // leaf boxes of the device node copies (see k_fill_blas_leaves) and the wide layout of the
+    // G-buffer traversal: BLAS node -> primitive offset / node range of the mesh that owns it,
+    // from the instances' mesh indices
+    const uint32_t n_blas = d->asset_nodes.count, n_tlas = d->instance_nodes.count;
+    std::vector<uint32_t> prim_offset(n_blas, HK_U32_MAX), node_base(n_blas, HK_U32_MAX), node_count(n_blas, 0);
+    const hk_instance* inst = (const hk_instance*)d->instances.data;
+    const hk_node* blas = (const hk_node*)d->asset_nodes.data;
+    const hk_node* tlas = (const hk_node*)d->instance_nodes.data;
+    for (uint32_t k = 0; k < d->instances.count; ++k) {
+        const hk_mesh_index& m = inst[k].mesh;
+        if ((size_t)m.node[0] + m.node[1] > n_blas) return fail(c, HK_ERR_INVALID, "instance mesh node range outside asset nodes");
+        for (uint32_t j = 0; j < m.node[1]; ++j) {
+            prim_offset[m.node[0] + j] = m.primitive;
+            node_base[m.node[0] + j] = m.node[0];
+            node_count[m.node[0] + j] = m.node[1];
         }
-        uint32_t* d_off = nullptr;
-        HK_HIP(c, hipMalloc(&d_off, (size_t)n_blas * 4));
-        HK_HIP(c, hipMemcpy(d_off, prim_offset.data(), (size_t)n_blas * 4, hipMemcpyHostToDevice));
-        launch_fill_leaves((hk_node*)c->buf[2], n_blas, d_off, (const hk_primitive*)c->buf[1], (hk_node*)c->buf[5],
-                           c->count[5], (const hk_instance*)c->buf[4], c->count[4], c->stream);
-        HK_HIP(c, hipGetLastError());
-        HK_HIP(c, hipStreamSynchronize(c->stream));
-        release(d_off);
     }
+    // stack bound of closest_hit_ordered: pushes along a path <= inner subtree starts on it
+    auto depth = [](const hk_node* f, uint32_t count) {
+        std::vector<uint32_t> dep(count + 1, 0);
+        uint32_t best = 0;
+        for (uint32_t p = count; p-- > 0;) {
+            if (f[p].entry_index >= HK_BVH_LEAF_FLAG) continue;
+            uint32_t q = f[p].exit_index;
+            uint32_t dl = p + 1 < count ? dep[p + 1] : 0, dr = q < count && q + 1 < count ? dep[q + 1] : 0;
+            dep[p] = 1 + (dl > dr ? dl : dr);
+        }
+        for (uint32_t p = 0; p < count; ++p) best = dep[p] > best ? dep[p] : best;
+        return best;
+    };
+    uint32_t blas_depth = 0;
+    for (uint32_t k = 0; k < d->instances.count; ++k) {
+        const hk_mesh_index& m = inst[k].mesh;
+        uint32_t dd = depth(blas + m.node[0], m.node[1]);
+        blas_depth = dd > blas_depth ? dd : blas_depth;
+    }
+    c->gb_stack_need = depth(tlas, n_tlas) + blas_depth;
+    uint32_t* d_aux = nullptr;
+    HK_HIP(c, hipMalloc(&d_aux, (size_t)(n_blas ? n_blas : 1) * 12));
+    if (n_blas) {
+        HK_HIP(c, hipMemcpy(d_aux, prim_offset.data(), (size_t)n_blas * 4, hipMemcpyHostToDevice));
+        HK_HIP(c, hipMemcpy(d_aux + n_blas, node_base.data(), (size_t)n_blas * 4, hipMemcpyHostToDevice));
+        HK_HIP(c, hipMemcpy(d_aux + 2 * (size_t)n_blas, node_count.data(), (size_t)n_blas * 4, hipMemcpyHostToDevice));
+    }
+    launch_fill_leaves((hk_node*)c->buf[2], n_blas, d_aux, (const hk_primitive*)c->buf[1], (hk_node*)c->buf[5],
+                       n_tlas, (const hk_instance*)c->buf[4], c->count[4], c->stream);
+    HK_HIP(c, hipGetLastError());
+    release(c->blas_wide);
+    release(c->tlas_wide);
+    HK_HIP(c, hipMalloc(&c->blas_wide, (size_t)(n_blas ? n_blas : 1) * 64));
+    HK_HIP(c, hipMalloc(&c->tlas_wide, (size_t)(n_tlas ? n_tlas : 1) * 64));
+    launch_build_wide((const hk_node*)c->buf[2], n_blas, d_aux + n_blas, d_aux + 2 * (size_t)n_blas, c->blas_wide,
+                      c->stream);
+    launch_build_wide((const hk_node*)c->buf[5], n_tlas, nullptr, nullptr, c->tlas_wide, c->stream);
+    HK_HIP(c, hipGetLastError());
+    HK_HIP(c, hipStreamSynchronize(c->stream));
+    release(d_aux);
     c->has_scene = true;
     return HK_OK;
 }
@@ -487,6 +531,8 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     int rc = check_ready(c, true);
     if (rc) return rc;
     if (!in) return fail(c, HK_ERR_INVALID, "null frame inputs");
+    if (c->gb_stack_need > (uint32_t)GB_STACK)
+        return fail(c, HK_ERR_INVALID, "scene BVH too deep for the G-buffer traversal stack (TLAS + BLAS depth > 64)");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
     FrameArgs A = frame_args(c, nullptr, in);

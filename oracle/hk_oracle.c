@@ -23,6 +23,7 @@
 #include "../include/hk_math.h"
 
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -1409,6 +1410,141 @@ static float ndc_depth(const float* view_proj, v3 p)
     v4 clip = mat4_mul(view_proj, V4(p.x, p.y, p.z, 1.0f));
     return clip.z / clip.w;
 }
+/* ---- G-buffer visibility: ordered closest-hit traversal (this build's primary-ray pass) ----
+ * The reference rasterises the G-buffer (prepass.wgsl:84-100); this build traces one primary ray
+ * per pixel instead, so its visibility rule is the build's own and is defined here, once, for
+ * the oracle and for the HIP kernel (hk_device.h closest_hit_ordered), which must agree bit for
+ * bit.  It walks the same flattened TLAS/BLAS (bvh 0.7.1 flatten: the subtree of an inner node
+ * starts with the box node of its left child, whose subtree follows it; the box node of the
+ * right child is at that box node's exit index) with the tests of light.wgsl:344-486:
+ *   - a subtree starting at a leaf entry is a candidate: BLAS leaf -> slab test of its
+ *     triangle's box (min/max of the 3 vertices), then Moller-Trumbore; TLAS leaf -> slab test of
+ *     the instance's min/max, then the instance's BLAS from its position 0 (no root box test,
+ *     as in the reference walk); a test passes iff its distance < best;
+ *   - an inner subtree has two children (box node, subtree after it); a child is entered iff
+ *     its box's slab distance t < best; with both entered, the smaller t first (left on ties)
+ *     and the other is pushed with its t and dropped on pop if t >= best by then;
+ *   - a triangle replaces the best hit iff d < best (the first found wins ties).
+ * BLAS indices are mesh-local (offset by mesh.node[0], light.wgsl:404-405).  The stack never
+ * holds more entries than TLAS depth + BLAS depth (HKO_GB_STACK, checked). */
+#define HKO_GB_STACK 64
+typedef struct { uint32_t node[HKO_GB_STACK]; float t[HKO_GB_STACK]; int sp; } GbStack;
+static void gb_push(GbStack* s, uint32_t n, float t)
+{
+    if (s->sp >= HKO_GB_STACK) {
+        fprintf(stderr, "hk_oracle: G-buffer traversal stack overflow (BVH deeper than %d)\n", HKO_GB_STACK);
+        abort();
+    }
+    s->node[s->sp] = n;
+    s->t[s->sp] = t;
+    s->sp++;
+}
+/* pop the next entry above `base` whose t is still < best; returns 0 when none is left */
+static int gb_pop(GbStack* s, int base, float best, uint32_t* n)
+{
+    while (s->sp > base) {
+        s->sp--;
+        if (s->t[s->sp] < best) {
+            *n = s->node[s->sp];
+            return 1;
+        }
+    }
+    return 0;
+}
+/* the two children of the inner subtree at `p`: (box node, subtree start) pairs */
+static void gb_children(const hk_node* nodes, uint32_t base, uint32_t p, uint32_t* lb, uint32_t* rb)
+{
+    *lb = p;
+    *rb = base + nodes[p].exit_index;
+}
+static void gb_descend(GbStack* s, const Ray* ray, const hk_node* nodes, uint32_t base, uint32_t* p, float best,
+                       int* go)
+{
+    uint32_t lb, rb;
+    gb_children(nodes, base, *p, &lb, &rb);
+    Aabb la = {ld3(nodes[lb].min), ld3(nodes[lb].max)}, ra = {ld3(nodes[rb].min), ld3(nodes[rb].max)};
+    float tl = intersects_aabb(ray, la), tr = intersects_aabb(ray, ra);
+    int hl = tl < best, hr = tr < best;
+    *go = 1;
+    if (hl && hr) {
+        if (tr < tl) {
+            gb_push(s, lb + 1, tl);
+            *p = rb + 1;
+        } else {
+            gb_push(s, rb + 1, tr);
+            *p = lb + 1;
+        }
+    } else if (hl) {
+        *p = lb + 1;
+    } else if (hr) {
+        *p = rb + 1;
+    } else {
+        *go = 0;
+    }
+}
+static void closest_bottom_ordered(const hko_ctx* c, GbStack* s, Hit* hit, const Ray* ray, const hk_mesh_index* mesh,
+                                   uint32_t instance_index)
+{
+    const int sbase = s->sp;
+    const uint32_t base = mesh->node[0];
+    if (mesh->node[1] == 0) return;
+    uint32_t p = base;
+    for (;;) {
+        const hk_node* node = &c->asset_nodes[p];
+        int go = 0;
+        if (node->entry_index >= HK_BVH_LEAF_FLAG) {
+            uint32_t primitive_index = mesh->primitive + node->entry_index - HK_BVH_LEAF_FLAG;
+            const hk_primitive_vertex* v = c->primitives[primitive_index].vertices;
+            v3 a = ld3(v[0].position), e = ld3(v[1].position), d = ld3(v[2].position);
+            Aabb box = {min3(a, min3(e, d)), max3(a, max3(e, d))};
+            if (intersects_aabb(ray, box) < hit->intersection.distance) {
+                Intersection is = intersects_triangle(ray, v);
+                if (is.distance < hit->intersection.distance) {
+                    hit->intersection = is;
+                    hit->primitive_index = primitive_index;
+                    hit->instance_index = instance_index;
+                }
+            }
+        } else {
+            gb_descend(s, ray, c->asset_nodes, base, &p, hit->intersection.distance, &go);
+        }
+        if (go) continue;
+        if (!gb_pop(s, sbase, hit->intersection.distance, &p)) return;
+    }
+}
+static Hit closest_hit_ordered(const hko_ctx* c, const Ray* ray)
+{
+    Hit hit;
+    hit.intersection.uv = V2(0, 0);
+    hit.intersection.distance = HK_F32_MAX;
+    hit.instance_index = HK_U32_MAX;
+    hit.primitive_index = HK_U32_MAX;
+    if (c->n_instance_nodes == 0) return hit;
+    GbStack s;
+    s.sp = 0;
+    uint32_t p = 0;
+    for (;;) {
+        const hk_node* node = &c->instance_nodes[p];
+        int go = 0;
+        if (node->entry_index >= HK_BVH_LEAF_FLAG) {
+            uint32_t instance_index = node->entry_index - HK_BVH_LEAF_FLAG;
+            const hk_instance* instance = &c->instances[instance_index];
+            Aabb box = {ld3(instance->min), ld3(instance->max)};
+            if (intersects_aabb(ray, box) < hit.intersection.distance) {
+                Ray r;
+                r.origin = instance_position_world_to_local(instance, ray->origin);
+                r.direction = instance_direction_world_to_local(instance, ray->direction);
+                r.inv_direction = inv3(r.direction);
+                closest_bottom_ordered(c, &s, &hit, &r, &instance->mesh, instance_index);
+            }
+        } else {
+            gb_descend(&s, ray, c->instance_nodes, 0, &p, hit.intersection.distance, &go);
+        }
+        if (go) continue;
+        if (!gb_pop(&s, 0, hit.intersection.distance, &p)) return hit;
+    }
+}
+
 static v3 primary_direction(const hk_view* view, float px, float py, const uint32_t* size)
 {
     float ndc_x = (px / (float)size[0]) * 2.0f - 1.0f;
@@ -1427,7 +1563,8 @@ static void gbuffer_pixel(const hko_ctx* c, Counts* cnt, const hk_frame_inputs* 
     ray.inv_direction = inv3(ray.direction);
     cnt->primary++;
     Counts dummy = {0, 0, 0};
-    Hit hit = traverse_top(c, &dummy, &ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+    (void)dummy;
+    Hit hit = closest_hit_ordered(c, &ray);
     float* gp = c->g_position + 4 * idx;
     float* gd = c->g_depth_gradient + 2 * idx;
     float* gi = c->g_instance_material + 2 * idx;

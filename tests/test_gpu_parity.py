@@ -223,3 +223,19 @@ def test_hardware_f16_conversion_matches_software_rne():
     # NaN stays NaN (quiet; payloads are canonicalised everywhere they are compared)
     g = got[nan]
     assert ((g & 0x7C00) == 0x7C00).all() and ((g & 0x03FF) != 0).all()
+
+
+@pytest.mark.parametrize("scene_fn,size", [("scene", (480, 270)), ("city", (480, 270)), ("cornell", (256, 256))])
+def test_gbuffer_ordered_traversal_matches_oracle(scene_fn, size):
+    """The primary-ray G-buffer (ordered closest-hit traversal over the wide BVH layout) against
+    the oracle's restatement of the same rule, on every G-buffer plane."""
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    w, h = size
+    scene, cam, lights, r, o = _setup(w, h, HikariSettings(upscale=Upscale.SMAA_TU_1_0), scene_fn)
+    fi = frame_inputs(0, cam, lights, w, h)
+    r.render_gbuffer(fi)
+    o.render_gbuffer(fi)
+    for oid in range(11, 16):
+        m = mismatch_report(canon_plane(oid, r.output(oid)), canon_plane(oid, o.output(oid)), f"output {oid}")
+        assert not m, m
+    assert r.counters()["primary"] == o.counters()["primary"] == w * h
