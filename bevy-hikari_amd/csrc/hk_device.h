@@ -90,6 +90,9 @@ constexpr uint32_t DONT_EXCLUDE = 0xFFFFFFFFu;
 constexpr uint32_t DONT_SAMPLE_EMISSIVE = 0x80000000u;
 
 // ------------------------------------------------------------------ kernel parameter blocks
+// Scene arrays in Scene declaration order: vertices, primitives, asset_nodes, alias_table,
+// instances, instance_nodes, materials, emissive_nodes, emissives, blas_wide, tlas_wide.
+constexpr int SCENE_ARRAYS = 11;
 struct Scene {
     const hk_vertex* vertices;
     const hk_primitive* primitives;
@@ -104,7 +107,27 @@ struct Scene {
     // G-buffer traversal layout (k_build_wide): per subtree start, both child boxes + starts
     const float4* blas_wide;
     const float4* tlas_wide;
+    // byte sizes of the arrays above, in declaration order (LDS staging, stage_scene)
+    uint32_t bytes[SCENE_ARRAYS];
 };
+
+// ------------------------------------------------------------------ LDS scene staging
+// Small scenes (cornell: ~9.5 KB of scene arrays) are copied into LDS by every workgroup of a
+// traversal kernel, so each dependent node / triangle / instance load of a walk is an LDS read
+// (~50 cycles) instead of an L2 hit (~200).  A plan lists the arrays a kernel reads.
+constexpr uint32_t LDS_SCENE_MAX = 32768;
+enum : int { PLAN_LIGHT = 0, PLAN_GBUFFER = 1 };
+__host__ __device__ constexpr bool plan_has(int plan, int k)
+{
+    return plan == PLAN_LIGHT ? k < 9 : (k == 0 || k == 1 || k == 4 || k == 9 || k == 10);
+}
+__host__ __device__ inline uint32_t stage_bytes(const uint32_t* bytes, int plan)
+{
+    uint32_t total = 0;
+    for (int k = 0; k < 11; ++k)
+        if (plan_has(plan, k)) total += (bytes[k] + 15u) & ~15u;
+    return total;
+}
 
 // Frame-uniform + view + lights constants (view.rs:105-123, mesh_view_bindings.wgsl).
 struct Frame {
@@ -150,6 +173,40 @@ struct Counters {
     unsigned long long* emitter;
     unsigned long long* primary;
 };
+
+template <int PLAN>
+HKD Scene stage_scene(const Scene& g, uint32_t* lds)
+{
+    const uint32_t* src[SCENE_ARRAYS] = {
+        (const uint32_t*)g.vertices,       (const uint32_t*)g.primitives, (const uint32_t*)g.asset_nodes,
+        (const uint32_t*)g.alias_table,    (const uint32_t*)g.instances,  (const uint32_t*)g.instance_nodes,
+        (const uint32_t*)g.materials,      (const uint32_t*)g.emissive_nodes, (const uint32_t*)g.emissives,
+        (const uint32_t*)g.blas_wide,      (const uint32_t*)g.tlas_wide};
+    uint32_t* dst[SCENE_ARRAYS];
+    uint32_t off = 0;
+#pragma unroll
+    for (int k = 0; k < SCENE_ARRAYS; ++k) {
+        dst[k] = lds + off;
+        if (!plan_has(PLAN, k)) continue;
+        const uint32_t words = g.bytes[k] >> 2;
+        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) dst[k][i] = src[k][i];
+        off += (words + 3u) & ~3u;
+    }
+    __syncthreads();
+    Scene s = g;
+    if (plan_has(PLAN, 0)) s.vertices = (const hk_vertex*)dst[0];
+    if (plan_has(PLAN, 1)) s.primitives = (const hk_primitive*)dst[1];
+    if (plan_has(PLAN, 2)) s.asset_nodes = (const hk_node*)dst[2];
+    if (plan_has(PLAN, 3)) s.alias_table = (const hk_alias_entry*)dst[3];
+    if (plan_has(PLAN, 4)) s.instances = (const hk_instance*)dst[4];
+    if (plan_has(PLAN, 5)) s.instance_nodes = (const hk_node*)dst[5];
+    if (plan_has(PLAN, 6)) s.materials = (const hk_material*)dst[6];
+    if (plan_has(PLAN, 7)) s.emissive_nodes = (const hk_node*)dst[7];
+    if (plan_has(PLAN, 8)) s.emissives = (const hk_emissive*)dst[8];
+    if (plan_has(PLAN, 9)) s.blas_wide = (const float4*)dst[9];
+    if (plan_has(PLAN, 10)) s.tlas_wide = (const float4*)dst[10];
+    return s;
+}
 
 // ------------------------------------------------------------------ f16 (hardware)
 // v_cvt_f16_f32 rounds to nearest-even with f16 denormals kept (default MODE), which is the

@@ -202,6 +202,14 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.sc.n_emissive_nodes = c->count[7];
     A.sc.blas_wide = c->blas_wide;
     A.sc.tlas_wide = c->tlas_wide;
+    {
+        const size_t elem[9] = {sizeof(hk_vertex), sizeof(hk_primitive), sizeof(hk_node), sizeof(hk_alias_entry),
+                                sizeof(hk_instance), sizeof(hk_node), sizeof(hk_material), sizeof(hk_node),
+                                sizeof(hk_emissive)};
+        for (int k = 0; k < 9; ++k) A.sc.bytes[k] = (uint32_t)std::min<size_t>((size_t)c->count[k] * elem[k], 0xFFFFFFF0u);
+        A.sc.bytes[9] = (uint32_t)std::min<size_t>((size_t)c->count[2] * 64, 0xFFFFFFF0u);
+        A.sc.bytes[10] = (uint32_t)std::min<size_t>((size_t)c->count[5] * 64, 0xFFFFFFF0u);
+    }
     Frame& F = A.F;
     hk_settings def;
     hk_settings_default(&def);

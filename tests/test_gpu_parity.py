@@ -44,8 +44,15 @@ def _compare_frame(r, o, frame, errors):
             errors.append(m)
 
 
+@pytest.fixture(params=["1", "0", "2"], ids=["lds_default", "lds_off", "lds_all"])
+def lds_mode(request, monkeypatch):
+    """HK_LDS_SCENE: scene arrays staged in LDS by the default kernels / none / every traversal kernel."""
+    monkeypatch.setenv("HK_LDS_SCENE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("size", [(64, 64), (96, 72)])
-def test_cornell_frames_bit_exact(size):
+def test_cornell_frames_bit_exact(size, lds_mode):
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     w, h = size
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
