@@ -17,6 +17,7 @@
 #include "../../include/hk_math.h"
 #include "../../include/hk_types.h"
 #include "../../include/hikari_amd.h"
+#include "../../include/hk_texture.h"
 
 namespace hk {
 
@@ -109,6 +110,11 @@ struct Scene {
     const float4* tlas_wide;
     // byte sizes of the arrays above, in declaration order (LDS staging, stage_scene)
     uint32_t bytes[SCENE_ARRAYS];
+    // material textures (hk_texture_upload; n_textures = 0: the NO_TEXTURE pipeline)
+    const hk_texture_desc* textures;
+    const uint32_t* texels;
+    const float* texture_lut;
+    uint32_t n_textures;
 };
 
 // ------------------------------------------------------------------ LDS scene staging
@@ -971,7 +977,16 @@ HKD f3 calculate_view(const Frame& F, f4 world_position)
     if (F.orthographic) return normalize(ld3(F.view_proj_z));
     return normalize(ld3(F.view_world_position) - xyz(world_position));
 }
-HKD Surface retreive_surface(const Scene& sc, uint32_t material_index)
+// light.wgsl:729-794: NO_TEXTURE variant when the scene has no textures, otherwise each material
+// texture id != U32_MAX modulates its factor with textureSampleLevel(.., uv, 0) (hk_texture.h)
+HKD f4 sample_material_texture(const Scene& sc, uint32_t id, f2 uv)
+{
+    float t[4];
+    hk_sample_texture(sc.textures + id, sc.texels, sc.texture_lut, uv.x, uv.y, t);
+    return mk4(t[0], t[1], t[2], t[3]);
+}
+HKD bool has_texture(const Scene& sc, uint32_t id) { return id != HK_U32_MAX && id < sc.n_textures; }
+HKD Surface retreive_surface(const Scene& sc, uint32_t material_index, f2 uv)
 {
     const hk_material& m = get_material(sc, material_index);
     Surface s;
@@ -979,15 +994,33 @@ HKD Surface retreive_surface(const Scene& sc, uint32_t material_index)
     s.emissive = mk4(m.emissive[0], m.emissive[1], m.emissive[2], m.emissive[3]);
     s.metallic = m.metallic;
     s.occlusion = 1.0f;
+    if (sc.n_textures) {
+        if (has_texture(sc, m.base_color_texture)) {
+            f4 t = sample_material_texture(sc, m.base_color_texture, uv);
+            s.base_color = mk4(s.base_color.x * t.x, s.base_color.y * t.y, s.base_color.z * t.z, s.base_color.w * t.w);
+        }
+        if (has_texture(sc, m.emissive_texture)) {
+            f4 t = sample_material_texture(sc, m.emissive_texture, uv);
+            s.emissive = mk4(s.emissive.x * t.x, s.emissive.y * t.y, s.emissive.z * t.z, s.emissive.w * t.w);
+        }
+        if (has_texture(sc, m.metallic_roughness_texture))
+            s.metallic = s.metallic * sample_material_texture(sc, m.metallic_roughness_texture, uv).x;
+        if (has_texture(sc, m.occlusion_texture)) s.occlusion = sample_material_texture(sc, m.occlusion_texture, uv).x;
+    }
     float pr = hk_clampf(m.perceptual_roughness, 0.089f, 1.0f);
     s.roughness = pr * pr;
     s.reflectance = m.reflectance;
     return s;
 }
-HKD f4 retreive_emissive(const Scene& sc, uint32_t material_index)
+HKD f4 retreive_emissive(const Scene& sc, uint32_t material_index, f2 uv)
 {
     const hk_material& m = get_material(sc, material_index);
-    return mk4(m.emissive[0], m.emissive[1], m.emissive[2], m.emissive[3]);
+    f4 e = mk4(m.emissive[0], m.emissive[1], m.emissive[2], m.emissive[3]);
+    if (sc.n_textures && has_texture(sc, m.emissive_texture)) {
+        f4 t = sample_material_texture(sc, m.emissive_texture, uv);
+        e = mk4(e.x * t.x, e.y * t.y, e.z * t.z, e.w * t.w);
+    }
+    return e;
 }
 HKD float F_Schlick(float f0, float f90, float VoH) { return f0 + (f90 - f0) * hk_pow(1.0f - VoH, 5.0f); }
 HKD f3 F_Schlick_vec(f3 f0, float f90, float VoH)
@@ -1079,7 +1112,7 @@ HKD f4 input_radiance(const Scene& sc, const Frame& F, const Ray& ray, const Hit
             amb = 1.0f;
         }
     } else if (sample_emissive == info.instance_index) {
-        radiance = emissive_radiance(retreive_emissive(sc, info.material_index));
+        radiance = emissive_radiance(retreive_emissive(sc, info.material_index, info.uv));
     }
     return mk4(radiance.x, radiance.y, radiance.z, 1.0f - amb);
 }

@@ -153,7 +153,8 @@ __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
     }
     f3 normal = load_normal(A.F, A.G, x, y);
     uint32_t material = f2u32(load_instance_material(A.F, A.G, x, y).y);
-    Surface surface = retreive_surface(A.sc, material);
+    const f4 velocity_uv = load_velocity_uv(A.F, A.G, x, y);
+    Surface surface = retreive_surface(A.sc, material, mk2(velocity_uv.z, velocity_uv.w));
     f3 view_direction = calculate_view(A.F, mk4(pd.x, pd.y, pd.z, 1.0f));
     f3 a = env_brdf(view_direction, normal, surface);
     store_rgba16f(albedo, idx, mk4(a.x, a.y, a.z, 1.0f));
@@ -271,7 +272,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     C.variance[idx] = variance_of(r);
     if (F.temporal_reuse > 0u) store_res(C.cur, idx, r);
 
-    Surface surface = retreive_surface(sc, im_y);
+    Surface surface = retreive_surface(sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
     f3 view_direction = calculate_view(F, position);
     f3 out = shading(F, view_direction, r.s.visible_normal, normalize(xyz(r.s.sample_position) - xyz(r.s.visible_position)),
                      surface, r.s.radiance);
@@ -354,7 +355,7 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
             bs.sample_normal = info.normal;
             if (hit.instance_index != HK_U32_MAX) {
                 f3 out = mk3(0, 0, 0);
-                surface = retreive_surface(sc, info.material_index);
+                surface = retreive_surface(sc, info.material_index, info.uv);
                 surface.roughness = 1.0f;
                 LightCandidate cand = select_light_candidate<true>(sc, F, bs.random, xyz(bs.sample_position),
                                                                    bs.sample_normal, info.instance_index, info, n_emitter);
@@ -403,7 +404,7 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
         s.sample_normal = info.normal;
         pdf = rs.w;
         if (hit.instance_index != HK_U32_MAX) {
-            surface = retreive_surface(sc, info.material_index);
+            surface = retreive_surface(sc, info.material_index, info.uv);
             surface.roughness = 1.0f;
             LightCandidate cand = select_light_candidate<true>(sc, F, s.random, xyz(s.sample_position), s.sample_normal,
                                                                info.instance_index, info, n_emitter);
@@ -435,7 +436,7 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
         int32_t py = f2i32(previous_uv.y * (float)F.s[1]);
         store_res(C.prev_spatial, s_index(F, px, py), r);
     }
-    surface = retreive_surface(sc, im_y);
+    surface = retreive_surface(sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
     f3 view_direction = calculate_view(F, position);
     f3 sample_radiance = shading(F, view_direction, s.visible_normal,
                                  normalize(xyz(s.sample_position) - xyz(s.visible_position)), surface, s.radiance);
@@ -512,7 +513,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     }
     uint32_t im_y = f2u32(load_instance_material(F, A.G, dx, dy).y);
     f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
-    Surface surface = retreive_surface(A.sc, im_y);
+    Surface surface = retreive_surface(A.sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
     bool use_spatial_variance = r.count <= 4.0f;
     f2 juv = jittered_uv(F, uv, 0.25f);
     f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);

@@ -47,6 +47,11 @@ struct hk_ctx {
     bool has_scene = false;
     uchar4* noise = nullptr;
     bool has_noise = false;
+    // material textures (hk_texture_upload)
+    hk_texture_desc* tex_desc = nullptr;
+    uint32_t* texels = nullptr;
+    float* tex_lut = nullptr;
+    uint32_t n_textures = 0;
 
     // sizes
     uint32_t S[2] = {0, 0}, s[2] = {0, 0};
@@ -202,6 +207,10 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.sc.n_emissive_nodes = c->count[7];
     A.sc.blas_wide = c->blas_wide;
     A.sc.tlas_wide = c->tlas_wide;
+    A.sc.textures = c->tex_desc;
+    A.sc.texels = c->texels;
+    A.sc.texture_lut = c->tex_lut;
+    A.sc.n_textures = c->n_textures;
     {
         const size_t elem[9] = {sizeof(hk_vertex), sizeof(hk_primitive), sizeof(hk_node), sizeof(hk_alias_entry),
                                 sizeof(hk_instance), sizeof(hk_node), sizeof(hk_material), sizeof(hk_node),
@@ -330,6 +339,9 @@ void hk_destroy(hk_ctx* c)
     for (int i = 0; i < 9; ++i) release(c->buf[i]);
     release(c->blas_wide);
     release(c->tlas_wide);
+    release(c->tex_desc);
+    release(c->texels);
+    release(c->tex_lut);
     release(c->noise);
     release(c->counters);
     for (auto& t : c->pending) {
@@ -423,6 +435,43 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
     HK_HIP(c, hipStreamSynchronize(c->stream));
     release(d_aux);
     c->has_scene = true;
+    return HK_OK;
+}
+
+int hk_texture_upload(hk_ctx* c, const hk_texture* t, uint32_t count)
+{
+    if (!c || (count && !t)) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    std::vector<hk_texture_desc> desc(count);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        if (!t[i].width || !t[i].height || !t[i].rgba8) return fail(c, HK_ERR_INVALID, "texture without texels");
+        if (t[i].format > HK_TEXTURE_RGBA8_UNORM || t[i].address_u > HK_ADDRESS_MIRROR_REPEAT ||
+            t[i].address_v > HK_ADDRESS_MIRROR_REPEAT || t[i].filter > HK_FILTER_LINEAR)
+            return fail(c, HK_ERR_INVALID, "unknown texture format / address mode / filter");
+        desc[i] = hk_texture_desc{(uint32_t)total, t[i].width, t[i].height, t[i].format, t[i].address_u,
+                                  t[i].address_v, t[i].filter, 0u};
+        total += (uint64_t)t[i].width * t[i].height;
+        if (total > 0xFFFFFFFFull) return fail(c, HK_ERR_INVALID, "more than 2^32 texels");
+    }
+    HK_HIP(c, hipStreamSynchronize(c->stream));
+    release(c->tex_desc);
+    release(c->texels);
+    c->n_textures = 0;
+    if (count == 0) return HK_OK;
+    if (!c->tex_lut) {
+        float lut[512];
+        hk_texture_build_lut(lut);
+        HK_HIP(c, hipMalloc(&c->tex_lut, sizeof(lut)));
+        HK_HIP(c, hipMemcpy(c->tex_lut, lut, sizeof(lut), hipMemcpyHostToDevice));
+    }
+    HK_HIP(c, hipMalloc(&c->tex_desc, count * sizeof(hk_texture_desc)));
+    HK_HIP(c, hipMemcpy(c->tex_desc, desc.data(), count * sizeof(hk_texture_desc), hipMemcpyHostToDevice));
+    HK_HIP(c, hipMalloc(&c->texels, total * 4));
+    for (uint32_t i = 0; i < count; ++i)
+        HK_HIP(c, hipMemcpy(c->texels + desc[i].offset, t[i].rgba8, (size_t)t[i].width * t[i].height * 4,
+                            hipMemcpyHostToDevice));
+    c->n_textures = count;
     return HK_OK;
 }
 

@@ -42,6 +42,17 @@ class hk_scene_desc(C.Structure):
                                        "instance_nodes", "materials", "emissive_nodes", "emissives")]
 
 
+class hk_texture(C.Structure):
+    """include/hikari_amd.h hk_texture (one GpuImage level 0 + its sampler)."""
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("format", C.c_uint32), ("address_u", C.c_uint32),
+                ("address_v", C.c_uint32), ("filter", C.c_uint32), ("rgba8", C.c_void_p)]
+
+
+TEXTURE_RGBA8_SRGB, TEXTURE_RGBA8_UNORM = 0, 1
+ADDRESS_CLAMP_TO_EDGE, ADDRESS_REPEAT, ADDRESS_MIRROR_REPEAT = 0, 1, 2
+FILTER_NEAREST, FILTER_LINEAR = 0, 1
+
+
 class hk_settings(C.Structure):
     _fields_ = [
         ("direct_validate_interval", C.c_uint32),
@@ -119,6 +130,7 @@ def lib() -> C.CDLL:
         "hk_settings_default": (None, [C.POINTER(hk_settings)]),
         "hk_scene_upload": (i32, [vp, C.POINTER(hk_scene_desc)]),
         "hk_set_noise": (i32, [vp, vp, u32, u32]),
+        "hk_texture_upload": (i32, [vp, vp, u32]),
         "hk_resize": (i32, [vp, u32, u32, C.c_float, u32, u32]),
         "hk_set_band_halo": (i32, [vp, u32]),
         "hk_band_info": (i32, [vp] + [C.POINTER(C.c_int32)] * 4),
@@ -159,7 +171,7 @@ def lib() -> C.CDLL:
 # symbols include/*.h declare (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
-    "hk_set_noise", "hk_resize", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
+    "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
     "hk_trace", "hk_selftest_f16", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",

@@ -30,6 +30,46 @@ def cornell():
     return scene, camera, lights
 
 
+def cornell_textured():
+    """cornell.rs with procedural material textures on every texture slot the integrator samples
+    (light.wgsl:748-794): sRGB checker base colours (repeat / linear and mirror-repeat / nearest),
+    a linear metallic-roughness gradient (clamp-to-edge), an occlusion ramp and an sRGB emissive
+    pattern on the light.  The reference scene has no textures; this exercises the textured
+    pipeline on the same geometry."""
+    from . import _abi
+    from .scene import Texture
+    scene, camera, lights = cornell()
+    rng = np.random.default_rng(0x48494B41)
+    y, x = np.mgrid[0:64, 0:64]
+    checker = (((x // 8) + (y // 8)) % 2).astype(np.uint8)
+    base = np.stack([np.where(checker, 230, 60), np.where(checker, 200, 90), np.where(checker, 170, 200),
+                     np.full_like(checker, 255)], axis=-1).astype(np.uint8)
+    noise = rng.integers(0, 256, (16, 16, 4), dtype=np.uint8)
+    noise[..., 3] = 255
+    grad = np.stack([np.tile(np.linspace(0, 255, 32, dtype=np.uint8), (32, 1))] * 3
+                    + [np.full((32, 32), 255, np.uint8)], axis=-1)
+    ramp = np.stack([np.repeat(np.linspace(80, 255, 8, dtype=np.uint8)[:, None], 8, axis=1)] * 4, axis=-1)
+    t_base = scene.add_texture(Texture(base, srgb=True, address_u=_abi.ADDRESS_REPEAT, address_v=_abi.ADDRESS_REPEAT,
+                                       filter=_abi.FILTER_LINEAR))
+    t_noise = scene.add_texture(Texture(noise, srgb=True, address_u=_abi.ADDRESS_MIRROR_REPEAT,
+                                        address_v=_abi.ADDRESS_REPEAT, filter=_abi.FILTER_NEAREST))
+    t_mr = scene.add_texture(Texture(grad, srgb=False, address_u=_abi.ADDRESS_CLAMP_TO_EDGE,
+                                     address_v=_abi.ADDRESS_CLAMP_TO_EDGE, filter=_abi.FILTER_LINEAR))
+    t_occ = scene.add_texture(Texture(ramp, srgb=False, address_u=_abi.ADDRESS_REPEAT,
+                                      address_v=_abi.ADDRESS_MIRROR_REPEAT, filter=_abi.FILTER_LINEAR))
+    for i, m in enumerate(scene.materials):
+        if max(m.emissive[:3]) > 0:
+            m.emissive_texture = t_noise
+            continue
+        m.base_color_texture = t_base if i % 2 == 0 else t_noise
+        if i % 3 == 0:
+            m.metallic = 0.8
+            m.metallic_roughness_texture = t_mr
+        if i % 3 == 1:
+            m.occlusion_texture = t_occ
+    return scene, camera, lights
+
+
 def _srgb(c):
     return tuple([srgb_to_linear(x) for x in c[:3]] + [c[3] if len(c) > 3 else 1.0])
 
@@ -170,4 +210,4 @@ def city():
     return scene, camera, make_lights(sun)
 
 
-SCENES = {"cornell": cornell, "scene": scene_rs, "city": city}
+SCENES = {"cornell": cornell, "cornell_textured": cornell_textured, "scene": scene_rs, "city": city}

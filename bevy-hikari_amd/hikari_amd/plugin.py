@@ -15,7 +15,7 @@ from typing import Optional
 import numpy as np
 
 from . import _abi
-from .scene import Scene, load_noise
+from .scene import Scene, load_noise, texture_array
 from .settings import HikariSettings, HikariUniversalSettings
 
 RESERVOIR_DTYPE = np.dtype([("radiance", "<u4", 2), ("random", "<u4", 2), ("visible_position", "<f4", 4),
@@ -55,6 +55,8 @@ class HikariRenderer:
     def upload_scene(self, scene: Scene) -> None:
         desc = scene.desc if scene.desc is not None else scene.build()
         _check(self.ctx, self._L.hk_scene_upload(self.ctx, C.byref(desc)), "hk_scene_upload")
+        tex = texture_array(scene.textures)
+        _check(self.ctx, self._L.hk_texture_upload(self.ctx, tex, len(scene.textures)), "hk_texture_upload")
 
     def set_noise(self, noise: Optional[np.ndarray] = None) -> None:
         n = np.ascontiguousarray(load_noise() if noise is None else noise, np.uint8)

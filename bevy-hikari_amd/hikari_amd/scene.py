@@ -190,18 +190,58 @@ class Mesh:
 
 @dataclass
 class StandardMaterial:
-    """Bevy 0.9 `StandardMaterial` defaults; colours given as linear RGBA."""
+    """Bevy 0.9 `StandardMaterial` defaults; colours given as linear RGBA.  Texture fields hold
+    indices into `Scene.textures` (the ids `MaterialTextures::id` assigns, material.rs:78-86)."""
 
     base_color: tuple = (1.0, 1.0, 1.0, 1.0)
     emissive: tuple = (0.0, 0.0, 0.0, 1.0)
     perceptual_roughness: float = 0.089
     metallic: float = 0.01
     reflectance: float = 0.5
+    base_color_texture: Optional[int] = None
+    emissive_texture: Optional[int] = None
+    metallic_roughness_texture: Optional[int] = None
+    normal_map_texture: Optional[int] = None
+    occlusion_texture: Optional[int] = None
 
     def record(self) -> bytes:
-        """GpuStandardMaterial std430 bytes (material.rs:162-199); no textures bound (NO_TEXTURE)."""
-        return struct.pack("<4fI3I4fIffIfIII", *self.base_color, U32_MAX, 0, 0, 0, *self.emissive, U32_MAX,
-                           self.perceptual_roughness, self.metallic, U32_MAX, self.reflectance, U32_MAX, U32_MAX, 0)
+        """GpuStandardMaterial std430 bytes (material.rs:162-199)."""
+        def tid(t):
+            return U32_MAX if t is None else int(t)
+        return struct.pack("<4fI3I4fIffIfIII", *self.base_color, tid(self.base_color_texture), 0, 0, 0,
+                           *self.emissive, tid(self.emissive_texture), self.perceptual_roughness, self.metallic,
+                           tid(self.metallic_roughness_texture), self.reflectance, tid(self.normal_map_texture),
+                           tid(self.occlusion_texture), 0)
+
+
+@dataclass
+class Texture:
+    """One Bevy `Image` as the renderer sees it: level-0 RGBA8 texels (rows, cols, 4) + sampler.
+    sRGB for base colour / emissive images, linear for metallic-roughness / occlusion."""
+
+    rgba8: np.ndarray
+    srgb: bool = True
+    address_u: int = _abi.ADDRESS_REPEAT
+    address_v: int = _abi.ADDRESS_REPEAT
+    filter: int = _abi.FILTER_LINEAR
+
+    def c_struct(self) -> "_abi.hk_texture":
+        a = np.ascontiguousarray(self.rgba8, np.uint8)
+        if a.ndim != 3 or a.shape[2] != 4:
+            raise ValueError("texture texels must be (rows, cols, 4) uint8")
+        self._keep = a
+        return _abi.hk_texture(a.shape[1], a.shape[0],
+                               _abi.TEXTURE_RGBA8_SRGB if self.srgb else _abi.TEXTURE_RGBA8_UNORM,
+                               self.address_u, self.address_v, self.filter, a.ctypes.data)
+
+
+def texture_array(textures) -> "C.Array":
+    """ctypes array of hk_texture for hk_texture_upload / hko_set_textures (keeps texels alive
+    through the Texture objects)."""
+    arr = (_abi.hk_texture * max(1, len(textures)))()
+    for i, t in enumerate(textures):
+        arr[i] = t.c_struct()
+    return arr
 
 
 def plane_mesh(size: float = 1.0) -> Mesh:
@@ -249,6 +289,7 @@ class Scene:
         self.meshes: List[Mesh] = []
         self.materials: List[StandardMaterial] = []
         self.instances: List[tuple] = []  # (mesh, material, 4x4 numpy)
+        self.textures: List[Texture] = []
         self._h = None
         self.desc: Optional[_abi.hk_scene_desc] = None
 
@@ -259,6 +300,10 @@ class Scene:
     def add_material(self, material: StandardMaterial) -> int:
         self.materials.append(material)
         return len(self.materials) - 1
+
+    def add_texture(self, texture: "Texture") -> int:
+        self.textures.append(texture)
+        return len(self.textures) - 1
 
     def add_instance(self, mesh: int, material: int, matrix: np.ndarray) -> int:
         self.instances.append((mesh, material, np.asarray(matrix, np.float64)))

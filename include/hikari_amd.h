@@ -11,6 +11,9 @@
  *   hk_scene_upload             the group-2 storage buffers written by
  *                               `MeshRenderAssets::set` (mesh.rs:43-58), `InstanceRenderAssets::set`
  *                               (instance.rs:82-99) and `MaterialRenderAssets` (material.rs:196-202)
+ *   hk_texture_upload           the material textures of `MaterialTextures` (material.rs:54-127), bound
+ *                               as group 3 `textures` / `samplers` (light.wgsl:15-19) when the
+ *                               scene has textures (the reference's non-NO_TEXTURE pipeline)
  *   hk_set_noise                the 16 blue-noise textures of `NoiseTextures` (lib.rs:189-219)
  *   hk_resize                   `prepare_light_textures` reallocation (light.rs:307-383), which
  *                               zero-fills the 10 reservoir buffers (light.rs:353-360)
@@ -36,6 +39,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include "hk_types.h"
+#include "hk_texture.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -166,6 +170,20 @@ void hk_settings_default(hk_settings* out);
 /* ---- resources ---- */
 int hk_scene_upload(hk_ctx* ctx, const hk_scene_desc* scene);
 int hk_set_noise(hk_ctx* ctx, const uint8_t* rgba8, uint32_t count, uint32_t size);
+
+/* Material textures: hk_material.*_texture ids index this array (material.rs:78-86, U32_MAX =
+ * none).  Each entry is a Bevy `GpuImage` level 0 (RGBA8, row-major, `width * height * 4`
+ * bytes; base colour / emissive images are sRGB, metallic-roughness / occlusion linear) with its
+ * `ImageSampler` (address mode per axis, magnification filter).  Sampling is defined in
+ * include/hk_texture.h.  Copies the texels; re-upload replaces; count 0 removes all. */
+typedef struct hk_texture {
+    uint32_t width, height;
+    uint32_t format;               /* HK_TEXTURE_RGBA8_SRGB / HK_TEXTURE_RGBA8_UNORM */
+    uint32_t address_u, address_v; /* HK_ADDRESS_CLAMP_TO_EDGE / _REPEAT / _MIRROR_REPEAT */
+    uint32_t filter;               /* HK_FILTER_NEAREST / HK_FILTER_LINEAR */
+    const uint8_t* rgba8;
+} hk_texture;
+int hk_texture_upload(hk_ctx* ctx, const hk_texture* textures, uint32_t count);
 /* physical size S = (width, height); integrator size s = ceil(S / ratio) (light.rs:318-319).
  * band_y0/band_rows select a horizontal band of the frame (multi-GPU); (0, height) = whole frame. */
 int hk_resize(hk_ctx* ctx, uint32_t width, uint32_t height, float upscale_ratio,

@@ -21,6 +21,7 @@
  */
 #include "hk_oracle.h"
 #include "../include/hk_math.h"
+#include "../include/hk_texture.h"
 
 #include <stdlib.h>
 #include <stdio.h>
@@ -123,6 +124,9 @@ struct hko_ctx {
     hk_material* materials; uint32_t n_materials;
     hk_node* emissive_nodes; uint32_t n_emissive_nodes;
     hk_emissive* emissives; uint32_t n_emissives;
+    /* material textures (hko_set_textures; none = the NO_TEXTURE pipeline) */
+    hk_texture_desc* tex_desc; uint32_t* texels; uint32_t n_textures;
+    float tex_lut[512];
     uint8_t noise[16 * 64 * 64 * 4];
 
     uint32_t S[2], s[2];
@@ -734,15 +738,37 @@ static v3 calculate_view(const Pass* P, v4 world_position, int is_orthographic)
 }
 static inline int is_orthographic(const Pass* P) { return P->in->view.projection[15] == 1.0f; }
 
+/* light.wgsl:729-794: the NO_TEXTURE variant when the scene has no textures, otherwise every
+ * texture id != U32_MAX modulates its factor by textureSampleLevel(.., uv, 0) (hk_texture.h) */
+static int has_texture(const hko_ctx* c, uint32_t id) { return id != HK_U32_MAX && id < c->n_textures; }
+static v4 sample_material_texture(const hko_ctx* c, uint32_t id, v2 uv)
+{
+    float t[4];
+    hk_sample_texture(c->tex_desc + id, c->texels, c->tex_lut, uv.x, uv.y, t);
+    return V4(t[0], t[1], t[2], t[3]);
+}
 static Surface retreive_surface(const Pass* P, uint32_t material_index, v2 uv)
 {
-    (void)uv; /* NO_TEXTURE variant (light.wgsl:729-747) */
-    const hk_material* m = get_material(P->c, material_index);
+    const hko_ctx* c = P->c;
+    const hk_material* m = get_material(c, material_index);
     Surface s;
     s.base_color = V4(m->base_color[0], m->base_color[1], m->base_color[2], m->base_color[3]);
     s.emissive = V4(m->emissive[0], m->emissive[1], m->emissive[2], m->emissive[3]);
     s.metallic = m->metallic;
     s.occlusion = 1.0f;
+    if (c->n_textures) {
+        if (has_texture(c, m->base_color_texture)) {
+            v4 t = sample_material_texture(c, m->base_color_texture, uv);
+            s.base_color = V4(s.base_color.x * t.x, s.base_color.y * t.y, s.base_color.z * t.z, s.base_color.w * t.w);
+        }
+        if (has_texture(c, m->emissive_texture)) {
+            v4 t = sample_material_texture(c, m->emissive_texture, uv);
+            s.emissive = V4(s.emissive.x * t.x, s.emissive.y * t.y, s.emissive.z * t.z, s.emissive.w * t.w);
+        }
+        if (has_texture(c, m->metallic_roughness_texture))
+            s.metallic = s.metallic * sample_material_texture(c, m->metallic_roughness_texture, uv).x;
+        if (has_texture(c, m->occlusion_texture)) s.occlusion = sample_material_texture(c, m->occlusion_texture, uv).x;
+    }
     float pr = hk_clampf(m->perceptual_roughness, 0.089f, 1.0f);
     s.roughness = pr * pr;
     s.reflectance = m->reflectance;
@@ -750,9 +776,14 @@ static Surface retreive_surface(const Pass* P, uint32_t material_index, v2 uv)
 }
 static v4 retreive_emissive(const Pass* P, uint32_t material_index, v2 uv)
 {
-    (void)uv;
-    const hk_material* m = get_material(P->c, material_index);
-    return V4(m->emissive[0], m->emissive[1], m->emissive[2], m->emissive[3]);
+    const hko_ctx* c = P->c;
+    const hk_material* m = get_material(c, material_index);
+    v4 e = V4(m->emissive[0], m->emissive[1], m->emissive[2], m->emissive[3]);
+    if (c->n_textures && has_texture(c, m->emissive_texture)) {
+        v4 t = sample_material_texture(c, m->emissive_texture, uv);
+        e = V4(e.x * t.x, e.y * t.y, e.z * t.z, e.w * t.w);
+    }
+    return e;
 }
 
 static float F_Schlick(float f0, float f90, float VoH)
@@ -1794,11 +1825,38 @@ hko_ctx* hko_create(const hk_scene_desc* sc, const uint8_t* noise, uint32_t widt
     return c;
 }
 
+int hko_set_textures(hko_ctx* c, const hk_texture* t, uint32_t count)
+{
+    free(c->tex_desc); free(c->texels);
+    c->tex_desc = NULL; c->texels = NULL; c->n_textures = 0;
+    if (count == 0) return 0;
+    uint64_t total = 0;
+    c->tex_desc = (hk_texture_desc*)calloc(count, sizeof(hk_texture_desc));
+    for (uint32_t i = 0; i < count; ++i) {
+        hk_texture_desc d = {(uint32_t)total, t[i].width, t[i].height, t[i].format, t[i].address_u, t[i].address_v,
+                             t[i].filter, 0u};
+        c->tex_desc[i] = d;
+        total += (uint64_t)t[i].width * t[i].height;
+    }
+    c->texels = (uint32_t*)malloc(total * 4 + 4);
+    for (uint32_t i = 0; i < count; ++i)
+        memcpy(c->texels + c->tex_desc[i].offset, t[i].rgba8, (size_t)t[i].width * t[i].height * 4);
+    hk_texture_build_lut(c->tex_lut);
+    c->n_textures = count;
+    return 0;
+}
+void hko_sample_texture(const hko_ctx* c, uint32_t id, const float* uv, uint32_t n, float* out)
+{
+    for (uint32_t i = 0; i < n; ++i)
+        hk_sample_texture(c->tex_desc + id, c->texels, c->tex_lut, uv[2 * i], uv[2 * i + 1], out + 4 * i);
+}
+
 void hko_destroy(hko_ctx* c)
 {
     if (!c) return;
     free(c->vertices); free(c->primitives); free(c->asset_nodes); free(c->alias_table); free(c->instances);
     free(c->instance_nodes); free(c->materials); free(c->emissive_nodes); free(c->emissives);
+    free(c->tex_desc); free(c->texels);
     free(c->g_position); free(c->g_normal); free(c->g_depth_gradient); free(c->g_instance_material); free(c->g_velocity_uv);
     free(c->albedo);
     for (int i = 0; i < 3; ++i) { free(c->variance[i]); free(c->render[i]); free(c->denoised[i]); }

@@ -32,6 +32,9 @@ typedef struct hko_ctx hko_ctx;
 hko_ctx* hko_create(const hk_scene_desc* scene, const uint8_t* noise, uint32_t width, uint32_t height,
                     float upscale_ratio, int threads);
 void hko_destroy(hko_ctx* ctx);
+/* material textures (hk_texture_upload) and a direct sampling entry for the KATs */
+int hko_set_textures(hko_ctx* ctx, const hk_texture* textures, uint32_t count);
+void hko_sample_texture(const hko_ctx* ctx, uint32_t id, const float* uv, uint32_t n, float* out);
 /* restrict every pass to rows [y0 - halo, y0 + rows + halo) (multi-rank band tests; ratio 1) */
 void hko_set_band(hko_ctx* ctx, int32_t y0, int32_t rows, int32_t halo);
 

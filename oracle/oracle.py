@@ -53,6 +53,8 @@ def lib() -> C.CDLL:
         "hko_cos": (f, [f]),
         "hko_f32_to_f16": (u32, [f]),
         "hko_f32_to_f16_array": (None, [C.c_void_p, C.c_size_t, C.c_void_p]),
+        "hko_set_textures": (C.c_int, [vp, vp, u32]),
+        "hko_sample_texture": (None, [vp, u32, vp, u32, vp]),
         "hko_hash": (u32, [u32]),
     }
     for name, (res, args) in sigs.items():
@@ -66,13 +68,29 @@ def lib() -> C.CDLL:
 class Oracle:
     """CPU restatement of one camera's integrator state (same API shape as HikariRenderer)."""
 
-    def __init__(self, scene_desc, noise: np.ndarray, width: int, height: int, ratio: float = 1.0, threads: int = 0):
+    def __init__(self, scene_desc, noise: np.ndarray, width: int, height: int, ratio: float = 1.0, threads: int = 0,
+                 textures=None):
         L = lib()
         self._L = L
         self._noise = np.ascontiguousarray(noise, np.uint8)
         self.ctx = L.hko_create(C.byref(scene_desc), self._noise.ctypes.data, width, height, ratio,
                                 threads or (os.cpu_count() or 1))
         self.width, self.height = width, height
+        if textures:
+            self.set_textures(textures)
+
+    def set_textures(self, textures):
+        """Material textures (a list of hikari_amd.Texture), as hk_texture_upload."""
+        from hikari_amd.scene import texture_array
+        self._textures = list(textures)
+        arr = texture_array(self._textures)
+        self._L.hko_set_textures(self.ctx, arr, len(self._textures))
+
+    def sample_texture(self, texture_id: int, uv: np.ndarray) -> np.ndarray:
+        uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+        out = np.empty((len(uv), 4), np.float32)
+        self._L.hko_sample_texture(self.ctx, texture_id, uv.ctypes.data, len(uv), out.ctypes.data)
+        return out
 
     def close(self):
         if getattr(self, "ctx", None):

@@ -23,7 +23,7 @@ def _setup(width, height, settings, scene_fn="cornell"):
     r.set_noise()
     r.upload_scene(scene)
     r.resize(width, height, settings.upscale.ratio())
-    o = Oracle(desc, load_noise(), width, height, settings.upscale.ratio())
+    o = Oracle(desc, load_noise(), width, height, settings.upscale.ratio(), textures=scene.textures)
     return scene, cam, lights, r, o
 
 
@@ -174,7 +174,7 @@ def _run_pair(scene_fn, w, h, settings, frames):
     desc = scene.build()
     ratio = settings.upscale.ratio()
     r = _gpu_factory(w, h, ratio)(scene, desc)
-    o = Oracle(desc, load_noise(), w, h, ratio)
+    o = Oracle(desc, load_noise(), w, h, ratio, textures=scene.textures)
     s = settings.to_c()
     errors = []
     for f in range(frames):
@@ -190,6 +190,15 @@ def _run_pair(scene_fn, w, h, settings, frames):
     assert not errors, "\n".join(errors[:20])
     assert r.counters() == o.counters()
     return r, o
+
+
+@pytest.mark.parametrize("ratio_setting", ["SMAA_TU_1_0", "SMAA_TU_2_0"])
+def test_textured_materials_bit_exact(ratio_setting):
+    """Textured pipeline (light.wgsl:748-794): sRGB / linear textures, all address modes and
+    filters, on base colour, emissive, metallic-roughness and occlusion slots."""
+    from hikari_amd import HikariSettings, Upscale
+    _run_pair("cornell_textured", 64, 48, HikariSettings(upscale=getattr(Upscale, ratio_setting),
+                                                         emissive_spatial_reuse=True, indirect_bounces=2), 5)
 
 
 def test_upscale_ratio_two_half_resolution_integrator():
