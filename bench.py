@@ -64,6 +64,11 @@ CONFIGS = {
     # configs[3]
     "city-4k": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True,
                     workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, row bands + RCCL all-gather"),
+    # configs[4]: 16 integrator sub-frames (each one reference frame) accumulated per displayed frame,
+    # one all-gather per displayed frame
+    "city-4k-16spp": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, spp=16,
+                          workload="examples/city.rs layout (City proxy houses) 3840x2160 16spp accumulation "
+                                   "(16 sub-frames per displayed frame), row bands + RCCL all-gather"),
 }
 
 
@@ -162,15 +167,24 @@ def main():
     band_t = torch.empty((band, W, 4), dtype=torch.float16, device="cuda")
     full_t = torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") if world > 1 else None
 
+    spp = cfg.get("spp", 1)
+    shown = hikari_amd._abi.OUT_TONE_MAPPED if spp == 1 else hikari_amd._abi.OUT_ACCUMULATED
+
     def step(f):
-        fi = frame_inputs(f, cam, lights, W, H)
-        r.render_gbuffer(fi, sp)
-        r.render_frame(s, fi, sp)
-        if st.denoise:
-            r.denoise(s, fi, sp)
-        r.tone_sum(s, sp)
+        # one displayed frame = spp integrator sub-frames, each exactly one reference frame
+        for k in range(spp):
+            fi = frame_inputs(f * spp + k, cam, lights, W, H)
+            r.render_gbuffer(fi, sp)
+            r.render_frame(s, fi, sp)
+            if st.denoise:
+                r.denoise(s, fi, sp)
+            r.tone_sum(s, sp)
+            if spp > 1:
+                r.accumulate(k == 0, sp)
+        if spp > 1:
+            r.resolve_accumulation(sp)
         if world > 1:
-            r.copy_output_rows(hikari_amd._abi.OUT_TONE_MAPPED, core0, core_rows, band_t.data_ptr(), False, sp)
+            r.copy_output_rows(shown, core0, core_rows, band_t.data_ptr(), False, sp)
             dist.all_gather_into_tensor(full_t, band_t)
 
     for f in range(args.warmup):
@@ -228,7 +242,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (static camera; reference assets: cornell.glb, blue noise)",
-            "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": 1,
+            "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": spp,
                        "rays_per_frame": int(rays // args.steps),
                        "parallelism": f"row-bands x{world} + RCCL all-gather" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -905,6 +905,31 @@ void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {
     hipLaunchKernelGGL(k_tone, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
 }
+// ------------------------------------------------------------------ sub-frame accumulation
+__global__ __launch_bounds__(256) void k_accumulate(const uint2* tone, float4* acc, uint32_t n, int reset)
+{
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    f4 t = load_rgba16f(tone, (int32_t)i);
+    float4 a = reset ? make_float4(0, 0, 0, 0) : acc[i];
+    acc[i] = make_float4(a.x + t.x, a.y + t.y, a.z + t.z, a.w + t.w);
+}
+__global__ __launch_bounds__(256) void k_resolve(const float4* acc, uint32_t n, float count, uint2* out)
+{
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    float4 a = acc[i];
+    store_rgba16f(out, (int32_t)i, mk4(a.x / count, a.y / count, a.z / count, a.w / count));
+}
+void launch_accumulate(const uint2* tone, float4* acc, uint32_t n, int reset, hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(k_accumulate, dim3((n + 255u) / 256u), dim3(256), 0, st, tone, acc, n, reset);
+}
+void launch_resolve(const float4* acc, uint32_t n, float count, uint2* out, hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(k_resolve, dim3((n + 255u) / 256u), dim3(256), 0, st, acc, n, count, out);
+}
+
 // ------------------------------------------------------------------ scene preparation
 // The reference's flattened leaves carry an empty AABB and the kernels recompute the box of the
 // leaf's triangle / instance before testing it (light.wgsl:411-412, 456-457).  At upload the

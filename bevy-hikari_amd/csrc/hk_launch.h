@@ -64,6 +64,8 @@ void launch_fill_leaves(hk_node* blas, uint32_t n_blas, const uint32_t* prim_off
                         hk_node* tlas, uint32_t n_tlas, const hk_instance* inst, uint32_t n_inst, hipStream_t st);
 void launch_build_wide(const hk_node* flat, uint32_t n, const uint32_t* node_base, const uint32_t* node_count,
                        float4* wide, hipStream_t st);
+void launch_accumulate(const uint2* tone, float4* acc, uint32_t n, int reset, hipStream_t st);
+void launch_resolve(const float4* acc, uint32_t n, float count, uint2* out, hipStream_t st);
 void launch_f16(const float* in, uint32_t n, uint16_t* out, hipStream_t st);
 void launch_trace(const Scene& sc, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl,
                   uint32_t n, uint32_t* hits, unsigned long long* top, hipStream_t st);

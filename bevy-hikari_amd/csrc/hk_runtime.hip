@@ -80,6 +80,9 @@ struct hk_ctx {
     int last_denoised_channels = 3;
     uint2* denoised[3] = {};
     uint2* tone = nullptr;
+    float4* accum = nullptr;      // sub-frame accumulator (hk_accumulate), allocated on first use
+    uint2* accum_out = nullptr;
+    uint32_t accum_n = 0;
     // counters (top, emitter, primary)
     unsigned long long* counters = nullptr;
 
@@ -136,6 +139,9 @@ void free_targets(hk_ctx* c)
     }
     release(c->geom);
     release(c->tone);
+    release(c->accum);
+    release(c->accum_out);
+    c->accum_n = 0;
     c->sized = false;
 }
 
@@ -713,6 +719,39 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     return HK_OK;
 }
 
+int hk_accumulate(hk_ctx* c, int reset, void* stream)
+{
+    int rc = check_ready(c, false);
+    if (rc) return rc;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
+    if (!c->accum) {
+        HK_HIP(c, hipMalloc(&c->accum, n * sizeof(float4)));
+        HK_HIP(c, hipMalloc(&c->accum_out, n * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->accum_out, 0, n * sizeof(uint2)));
+        reset = 1;
+    }
+    if (reset) c->accum_n = 0;
+    timed(c, "accumulate", st, [&] { launch_accumulate(c->tone, c->accum, (uint32_t)n, reset, st); });
+    HK_HIP(c, hipGetLastError());
+    c->accum_n += 1;
+    return HK_OK;
+}
+
+int hk_resolve_accumulation(hk_ctx* c, void* stream)
+{
+    int rc = check_ready(c, false);
+    if (rc) return rc;
+    if (!c->accum || c->accum_n == 0) return fail(c, HK_ERR_STATE, "nothing accumulated (hk_accumulate)");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
+    timed(c, "resolve", st, [&] { launch_resolve(c->accum, (uint32_t)n, (float)c->accum_n, c->accum_out, st); });
+    HK_HIP(c, hipGetLastError());
+    return HK_OK;
+}
+
 static void* output_ptr(hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* bpp)
 {
     uint32_t W = c->s[0], H = (uint32_t)c->s_rows, B = 8;
@@ -726,6 +765,7 @@ static void* output_ptr(hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* b
     case HK_OUT_DENOISED_DIRECT: case HK_OUT_DENOISED_EMISSIVE: case HK_OUT_DENOISED_INDIRECT:
         p = c->denoised[id - HK_OUT_DENOISED_DIRECT]; break;
     case HK_OUT_TONE_MAPPED: p = c->tone; break;
+    case HK_OUT_ACCUMULATED: p = c->accum_out; break;
     case HK_OUT_GBUF_POSITION: p = c->g_position; W = c->S[0]; H = (uint32_t)c->S_rows; B = 16; break;
     case HK_OUT_GBUF_NORMAL: p = c->g_normal; W = c->S[0]; H = (uint32_t)c->S_rows; B = 4; break;
     case HK_OUT_GBUF_DEPTH_GRADIENT: p = c->g_depth_gradient; W = c->S[0]; H = (uint32_t)c->S_rows; B = 8; break;

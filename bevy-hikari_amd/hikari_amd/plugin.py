@@ -93,6 +93,14 @@ class HikariRenderer:
     def tone_sum(self, settings: _abi.hk_settings, stream=None) -> None:
         _check(self.ctx, self._L.hk_tone_sum(self.ctx, C.byref(settings), stream), "hk_tone_sum")
 
+    def accumulate(self, reset: bool = False, stream=None) -> None:
+        """Add the tone-mapped output to the sub-frame accumulator (hk_accumulate)."""
+        _check(self.ctx, self._L.hk_accumulate(self.ctx, int(reset), stream), "hk_accumulate")
+
+    def resolve_accumulation(self, stream=None) -> None:
+        """Accumulator / sub-frame count -> OUT_ACCUMULATED (RGBA16F)."""
+        _check(self.ctx, self._L.hk_resolve_accumulation(self.ctx, stream), "hk_resolve_accumulation")
+
     # ---- readback
     def output_info(self, output_id: int):
         w, h, b = C.c_uint32(), C.c_uint32(), C.c_uint32()

@@ -146,7 +146,8 @@ typedef enum hk_output_id {
     HK_OUT_GBUF_INSTANCE_MATERIAL = 14, /* float2, S */
     HK_OUT_GBUF_VELOCITY_UV = 15, /* float4, S */
     HK_OUT_DENOISE_INTERNAL_VARIANCE = 16, /* R32F, s (last channel denoised) */
-    HK_OUT_COUNT = 17
+    HK_OUT_ACCUMULATED = 17,      /* RGBA16F, s: hk_resolve_accumulation */
+    HK_OUT_COUNT = 18
 } hk_output_id;
 
 /* Reservoir buffer ids 0..9 as allocated by light.rs:350-361; the channel pairs
@@ -170,6 +171,13 @@ void hk_settings_default(hk_settings* out);
 /* ---- resources ---- */
 int hk_scene_upload(hk_ctx* ctx, const hk_scene_desc* scene);
 int hk_set_noise(hk_ctx* ctx, const uint8_t* rgba8, uint32_t count, uint32_t size);
+
+/* Sub-frame accumulation (N integrator sub-frames per displayed frame, each
+ * exactly one reference frame): hk_accumulate adds the current tone-mapped output (HK_OUT_TONE_MAPPED)
+ * to an f32 RGBA accumulator, restarting it when reset != 0; hk_resolve_accumulation writes
+ * accumulator / count (RGBA16F) to HK_OUT_ACCUMULATED, the plane a displayed frame all-gathers. */
+int hk_accumulate(hk_ctx* ctx, int reset, void* stream);
+int hk_resolve_accumulation(hk_ctx* ctx, void* stream);
 
 /* Material textures: hk_material.*_texture ids index this array (material.rs:78-86, U32_MAX =
  * none).  Each entry is a Bevy `GpuImage` level 0 (RGBA8, row-major, `width * height * 4`

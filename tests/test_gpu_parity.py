@@ -255,3 +255,27 @@ def test_gbuffer_ordered_traversal_matches_oracle(scene_fn, size):
         m = mismatch_report(canon_plane(oid, r.output(oid)), canon_plane(oid, o.output(oid)), f"output {oid}")
         assert not m, m
     assert r.counters()["primary"] == o.counters()["primary"] == w * h
+
+
+def test_subframe_accumulation_matches_numpy():
+    """hk_accumulate / hk_resolve_accumulation (config 5): f32 running sum of the tone-mapped
+    RGBA16F sub-frames, divided by the count and rounded to f16 (numpy restatement, bit-exact)."""
+    from hikari_amd import HikariSettings, Upscale, _abi, frame_inputs
+    w, h = 48, 32
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
+    scene, cam, lights, r, o = _setup(w, h, st)
+    s = st.to_c()
+    acc = np.zeros((h, w, 4), np.float32)
+    for f in range(5):
+        fi = frame_inputs(f, cam, lights, w, h)
+        r.render_gbuffer(fi)
+        r.render_frame(s, fi)
+        r.denoise(s, fi)
+        r.tone_sum(s)
+        r.accumulate(reset=(f == 0))
+        t = r.output(_abi.OUT_TONE_MAPPED).view(np.float16).reshape(h, w, 4).astype(np.float32)
+        acc = (acc + t).astype(np.float32)
+    r.resolve_accumulation()
+    got = r.output(_abi.OUT_ACCUMULATED).view(np.uint16).reshape(h, w, 4)
+    want = (acc / np.float32(5.0)).astype(np.float32).astype(np.float16).view(np.uint16)
+    assert np.array_equal(got, want)
