@@ -479,7 +479,7 @@ HKD void temporal_restir(Reservoir& r, const Sample& s, float w_new, uint32_t ma
 }
 HKD float variance_of(const Reservoir& r)
 {
-    float variance = r.w2_sum / r.count - hk_pow(r.w_sum / r.count, 2.0f);
+    float variance = r.w2_sum / r.count - hk_pow2(r.w_sum / r.count);
     variance = r.count < 1.0f ? variance : variance / r.count;
     return fminf(variance, MAX_VARIANCE);
 }
@@ -1022,10 +1022,10 @@ HKD f4 retreive_emissive(const Scene& sc, uint32_t material_index, f2 uv)
     }
     return e;
 }
-HKD float F_Schlick(float f0, float f90, float VoH) { return f0 + (f90 - f0) * hk_pow(1.0f - VoH, 5.0f); }
+HKD float F_Schlick(float f0, float f90, float VoH) { return f0 + (f90 - f0) * hk_pow5(1.0f - VoH); }
 HKD f3 F_Schlick_vec(f3 f0, float f90, float VoH)
 {
-    float k = hk_pow(1.0f - VoH, 5.0f);
+    float k = hk_pow5(1.0f - VoH);
     return mk3(f0.x + (f90 - f0.x) * k, f0.y + (f90 - f0.y) * k, f0.z + (f90 - f0.z) * k);
 }
 HKD f3 EnvBRDFApprox(f3 f0, float pr, float NoV)
@@ -1058,7 +1058,7 @@ HKD ShadeCtx shade_ctx(const Frame& F, f3 V, f3 N, const Surface& s)
     c.diffuse_color = base * (1.0f - s.metallic);
     c.roughness = s.roughness;
     c.NdotV = fmaxf(dot(N, V), 0.0001f);
-    c.pow5_view = hk_pow(1.0f - c.NdotV, 5.0f);  // F_Schlick(1, f90, NdotV) of Fd_Burley
+    c.pow5_view = hk_pow5(1.0f - c.NdotV);  // F_Schlick(1, f90, NdotV) of Fd_Burley
     float a2 = s.roughness * s.roughness;
     c.smith_view = sqrtf((c.NdotV - a2 * c.NdotV) * c.NdotV + a2);  // lambdaV's root
     // ambient() (light.wgsl:820-833)

@@ -725,7 +725,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         const int32_t sidx = s_index(F, sx, sy);
         const float4 t0 = D.geom[2 * sidx];
         const float si = D.geom[2 * sidx + 1].x;
-        const float w_normal = hk_pow(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))), 16.0f);
+        const float w_normal = hk_pow16(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))));
         const float w_depth = hk_exp((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
         const float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
         const float w_geo = (w_normal * w_depth) * w_instance;

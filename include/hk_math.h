@@ -98,6 +98,34 @@ HK_HD float hk_log2(float x)
 /* WGSL pow(x, y) = exp2(y * log2(x)) for x >= 0 (NaN for x < 0). */
 HK_HD float hk_pow(float x, float y) { return hk_exp2(y * hk_log2(x)); }
 
+/* pow(x, n) for the literal integer exponents of the shaders — 5.0 in F_Schlick (Bevy
+ * pbr lighting), 2.0 in the reservoir variance (light.wgsl:976), 16.0 in the denoiser's normal
+ * weight (denoise.wgsl:48).  WGSL pins pow only to the accuracy of exp2(y * log2(x)), so the
+ * build evaluates these by repeated multiplication (<= 3 ulp for n = 5, well inside that bound)
+ * with hk_pow's domain: x < 0 or NaN -> NaN, +-0 -> +0, +inf -> +inf. */
+HK_HD float hk_pow2(float x)
+{
+    if (!(x >= 0.0f)) return hk_u2f(0x7FC00000u);
+    x = x + 0.0f; /* -0 -> +0 */
+    return x * x;
+}
+HK_HD float hk_pow5(float x)
+{
+    if (!(x >= 0.0f)) return hk_u2f(0x7FC00000u);
+    x = x + 0.0f;
+    float x2 = x * x;
+    return (x2 * x2) * x;
+}
+HK_HD float hk_pow16(float x)
+{
+    if (!(x >= 0.0f)) return hk_u2f(0x7FC00000u);
+    x = x + 0.0f;
+    float x2 = x * x;
+    float x4 = x2 * x2;
+    float x8 = x4 * x4;
+    return x8 * x8;
+}
+
 /* sin/cos with Cody-Waite reduction by pi/2 and Taylor kernels on [-pi/4, pi/4]. */
 HK_HD float hk_sin_kernel(float r)
 {

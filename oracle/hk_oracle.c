@@ -788,11 +788,11 @@ static v4 retreive_emissive(const Pass* P, uint32_t material_index, v2 uv)
 
 static float F_Schlick(float f0, float f90, float VoH)
 {
-    return f0 + (f90 - f0) * hk_pow(1.0f - VoH, 5.0f);
+    return f0 + (f90 - f0) * hk_pow5(1.0f - VoH);
 }
 static v3 F_Schlick_vec(v3 f0, float f90, float VoH)
 {
-    float k = hk_pow(1.0f - VoH, 5.0f);
+    float k = hk_pow5(1.0f - VoH);
     return V3(f0.x + (f90 - f0.x) * k, f0.y + (f90 - f0.y) * k, f0.z + (f90 - f0.z) * k);
 }
 static v3 fresnel(v3 f0, float LoH)
@@ -962,7 +962,7 @@ static float compute_jacobian(const Sample* q, const Sample* r)
 
 static float variance_of(const Reservoir* r)
 {
-    float variance = r->w2_sum / r->count - hk_pow(r->w_sum / r->count, 2.0f);
+    float variance = r->w2_sum / r->count - hk_pow2(r->w_sum / r->count);
     variance = r->count < 1.0f ? variance : variance / r->count;
     return hk_minf(variance, MAX_VARIANCE);
 }
@@ -1745,7 +1745,7 @@ static void denoise_pixel(const DPass* D, int32_t x, int32_t y)
         float sample_depth = load_position(c, tx, ty).w;
         float sample_instance = load_instance_material(c, tx, ty).x;
         float sample_luminance = lum3(irr);
-        float w_normal = hk_pow(hk_maxf(0.0f, dot3(normal, sample_normal)), 16.0f);
+        float w_normal = hk_pow16(hk_maxf(0.0f, dot3(normal, sample_normal)));
         float w_depth = hk_exp((-hk_absf(depth - sample_depth)) /
                                (hk_absf(dot2(depth_gradient, V2((float)ox, (float)oy))) + 0.01f));
         float w_instance = hk_maxf(0.0f, 1.0f - hk_absf(instance - sample_instance));
@@ -2124,6 +2124,7 @@ void hko_pack_reservoir_roundtrip(const float* f, hk_packed_reservoir* packed, f
     u[25] = q.s.sample_normal.x; u[26] = q.s.sample_normal.y; u[27] = q.s.sample_normal.z;
 }
 float hko_pow(float x, float y) { return hk_pow(x, y); }
+float hko_pow_int(float x, int n) { return n == 2 ? hk_pow2(x) : (n == 5 ? hk_pow5(x) : hk_pow16(x)); }
 float hko_exp2(float x) { return hk_exp2(x); }
 float hko_log2(float x) { return hk_log2(x); }
 float hko_sin(float x) { return hk_sin(x); }

@@ -59,6 +59,7 @@ void hko_intersects_triangle(const float* origin, const float* dir, const float*
                              const float* v2, float* out_uvt);
 void hko_pack_reservoir_roundtrip(const float* fields, hk_packed_reservoir* packed, float* unpacked);
 float hko_pow(float x, float y);
+float hko_pow_int(float x, int n); /* n in {2, 5, 16} */
 float hko_exp2(float x);
 float hko_log2(float x);
 float hko_sin(float x);

@@ -47,6 +47,7 @@ def lib() -> C.CDLL:
         "hko_intersects_triangle": (None, [vp, vp, vp, vp, vp, vp]),
         "hko_pack_reservoir_roundtrip": (None, [vp, vp, vp]),
         "hko_pow": (f, [f, f]),
+        "hko_pow_int": (f, [f, C.c_int]),
         "hko_exp2": (f, [f]),
         "hko_log2": (f, [f]),
         "hko_sin": (f, [f]),

@@ -400,3 +400,24 @@ def test_f16_conversion_matches_numpy_ieee_sweep():
     nan = np.isnan(vals)
     assert np.array_equal(got[~nan], want[~nan])
     assert ((got[nan] & 0x7C00) == 0x7C00).all() and ((got[nan] & 0x3FF) != 0).all()
+
+
+def test_integer_pow_accuracy_and_domain():
+    """hk_pow2/5/16 (literal-exponent pow): within a few ulp of the float64 power on [0, 4],
+    and the same special values as hk_pow (x < 0 / NaN -> NaN, +-0 -> +0, inf -> inf)."""
+    import math
+    import oracle as orc
+    L = orc.lib()
+    rng = np.random.default_rng(5)
+    xs = np.concatenate([rng.uniform(0, 1, 3000), rng.uniform(1, 4, 1000), [0.5, 1.0, 2.0]]).astype(np.float32)
+    for n, tol in ((2, 1), (5, 3), (16, 16)):
+        for x in xs:
+            got = np.float32(L.hko_pow_int(float(x), n))
+            want = float(x) ** n
+            if want == 0 or not math.isfinite(want) or want > 3.4e38:
+                continue
+            ulp = np.spacing(np.float32(want))
+            assert abs(float(got) - want) <= tol * ulp, (n, x, got, want)
+        assert math.isnan(L.hko_pow_int(-1.0, n)) and math.isnan(L.hko_pow_int(float("nan"), n))
+        assert math.copysign(1.0, L.hko_pow_int(-0.0, n)) == 1.0 and L.hko_pow_int(0.0, n) == 0.0
+        assert L.hko_pow_int(float("inf"), n) == float("inf")
