@@ -157,6 +157,15 @@ struct Frame {
     int32_t s_row0, s_rows;  // integrator-plane band
     int32_t count_y0, count_y1;    // global integrator rows whose rays are counted (the band's own rows)
     int32_t count_Sy0, count_Sy1;  // the same for the full-resolution G-buffer rows
+    // host-evaluated constants (same IEEE expressions, so bit-identical to computing them here)
+    float inv_S[2];                // 1 / S (jittered_uv texel size)
+    float inv_s[2];                // RN(1 / s): div_by() reciprocals of the integrator size
+    // spatial_reuse per-neighbour constants [EMISSIVE_LIT][i - 1] (light.wgsl:1568-1600):
+    // py = sqrt(i / COUNT) * RANGE, tap_interval = max(1, py / 5), tap_count = u32(py / tap_interval)
+    float sp_py[2][16];
+    float sp_tap_interval[2][16];
+    uint32_t sp_tap_count[2][16];
+    float sp_tap_t[7][6];          // [tap_count][j] = j / (tap_count + 1), the depth-march mix weight
 };
 
 // Row-major planes of the deferred (G-buffer) textures, band-local.
@@ -212,6 +221,22 @@ HKD Scene stage_scene(const Scene& g, uint32_t* lds)
     if (plan_has(PLAN, 9)) s.blas_wide = (const float4*)dst[9];
     if (plan_has(PLAN, 10)) s.tlas_wide = (const float4*)dst[10];
     return s;
+}
+
+// ------------------------------------------------------------------ division by a frame size
+// x / d for a per-frame constant divisor d (an image dimension) with r = RN(1/d) from the host:
+// q0 = x r, one correction brings q1 within 1 ulp of x / d, a second one (Markstein: r is the
+// correctly rounded reciprocal, q1 is within 1 ulp) rounds correctly — the same bits as the IEEE
+// divide for every x with a normal quotient (checked exhaustively over 2^31 patterns per divisor
+// by test_fast_division_by_frame_size_is_exact).  Signed zero kept.
+HKD float div_by(float x, float d, float r)
+{
+    const float q0 = x * r;
+    const float e0 = fmaf(-q0, d, x);
+    const float q1 = fmaf(e0, r, q0);
+    const float e1 = fmaf(-q1, d, x);
+    const float q2 = fmaf(e1, r, q1);
+    return x == 0.0f ? x * r : q2;
 }
 
 // ------------------------------------------------------------------ f16 (hardware)
@@ -319,10 +344,15 @@ HKD f2 coords_to_uv(int32_t x, int32_t y, const uint32_t* size)
 {
     return mk2(((float)x + 0.5f) / (float)size[0], ((float)y + 0.5f) / (float)size[1]);
 }
+// coords_to_uv on the integrator grid with div_by (same bits as the IEEE divide)
+HKD f2 coords_to_uv_s(const Frame& F, int32_t x, int32_t y)
+{
+    return mk2(div_by((float)x + 0.5f, (float)F.s[0], F.inv_s[0]), div_by((float)y + 0.5f, (float)F.s[1], F.inv_s[1]));
+}
 // light.wgsl:1007-1017 (jitter 0.25) / denoise.wgsl:37-41 (jitter 0.5)
 HKD f2 jittered_uv(const Frame& F, f2 uv, float amount)
 {
-    float tx = 1.0f / (float)F.S[0], ty = 1.0f / (float)F.S[1];
+    float tx = F.inv_S[0], ty = F.inv_S[1];  // 1 / S, evaluated on the host
     float ratio = F.upscale_ratio - 1.0f;
     float j = (F.number & 1u) == 0u ? -amount : amount;
     return mk2(uv.x + (j * tx) * ratio, uv.y + (j * ty) * ratio);

@@ -497,7 +497,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 {
     const Frame& F = A.F;
     constexpr uint32_t COUNT = EMISSIVE_LIT ? 8u : 16u;
-    constexpr float RANGE = EMISSIVE_LIT ? 10.0f : 20.0f;
     const int32_t idx = s_index(F, x, y);
     const f2 uv = coords_to_uv(x, y, F.s);
     int32_t dx, dy;
@@ -536,12 +535,12 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     const float srand = sum4(s.random);
     for (uint32_t i = 1u; i <= COUNT; i += 1u) {
         float px = HK_TAU * hk_fract(((float)i * HK_GOLDEN_RATIO + srand) + rf);
-        float py = sqrtf((float)i / (float)COUNT) * RANGE;
+        const float py = F.sp_py[EMISSIVE_LIT][i - 1u];  // sqrt(i / COUNT) * RANGE
         float sn, cs;
         hk_sincos(px, &sn, &cs);
         f2 offset = mk2(py * cs, py * sn);
         int32_t scx = f2i32(offset.x + (float)x), scy = f2i32(offset.y + (float)y);
-        f2 suv = coords_to_uv(scx, scy, F.s);
+        f2 suv = coords_to_uv_s(F, scx, scy);
         if (suv.x < 0.0f || suv.y < 0.0f || suv.x > 1.0f || suv.y > 1.0f) continue;
         int32_t sdx, sdy;
         jittered_coords(F, suv, sdx, sdy);
@@ -554,18 +553,21 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         f3 sample_direction = normalize(xyz(q.s.sample_position) - xyz(s.visible_position));
         if (dot(sample_direction, s.visible_normal) < 0.0f) continue;
 
-        float tap_interval = fmaxf(1.0f, py / 5.0f);
-        uint32_t tap_count = f2u32(py / tap_interval);
+        const float tap_interval = F.sp_tap_interval[EMISSIVE_LIT][i - 1u];  // max(1, py / 5)
+        const uint32_t tap_count = F.sp_tap_count[EMISSIVE_LIT][i - 1u];    // u32(py / tap_interval)
         bool occluded = false;
         float inv_len = 1.0f / sqrtf(dot(offset, offset));
         f2 dir = mk2(offset.x * inv_len, offset.y * inv_len);
         for (uint32_t j = 1u; j <= tap_count; j += 1u) {
             float tap_dist = (float)j * tap_interval;
-            f2 tuv = mk2(uv.x + (tap_dist * dir.x) / (float)F.s[0], uv.y + (tap_dist * dir.y) / (float)F.s[1]);
+            f2 tuv = mk2(uv.x + div_by(tap_dist * dir.x, (float)F.s[0], F.inv_s[0]),
+                         uv.y + div_by(tap_dist * dir.y, (float)F.s[1], F.inv_s[1]));
             int32_t tdx, tdy;
             jittered_coords(F, tuv, tdx, tdy);
             float tap_depth = win_depth(F, A.G, W, tdx, tdy);
-            float ref_depth = hk_mixf(depth, sample_depth, (float)j / (float)(tap_count + 1u));
+            // j / (tap_count + 1) from the host table (tap_count <= 5 for RANGE <= 20)
+            const float t = tap_count < 7u && j < 6u ? F.sp_tap_t[tap_count][j] : (float)j / (float)(tap_count + 1u);
+            float ref_depth = hk_mixf(depth, sample_depth, t);
             if (tap_depth > ref_depth + 0.00001f) {
                 occluded = true;
                 break;
@@ -720,7 +722,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         const int kk = k < 4 ? k : k + 1;  // skip the centre
         const int ox = kk % 3 - 1, oy = kk / 3 - 1;  // (-1,-1),(0,-1),(1,-1),(-1,0),(1,0),(-1,1),(0,1),(1,1)
         const int32_t sx = x + ox * step, sy = y + oy * step;
-        const f2 suv = coords_to_uv(sx, sy, F.s);
+        const f2 suv = coords_to_uv_s(F, sx, sy);
         if (uv_outside(suv)) continue;
         const int32_t sidx = s_index(F, sx, sy);
         const float4 t0 = D.geom[2 * sidx];
@@ -997,6 +999,25 @@ void launch_fill_leaves(hk_node* blas, uint32_t n_blas, const uint32_t* prim_off
                                    prim_offset, prims);
     if (n_tlas) hipLaunchKernelGGL(k_fill_tlas_leaves, dim3((n_tlas + 255u) / 256u), dim3(256), 0, st, tlas, n_tlas,
                                    inst, n_inst);
+}
+
+// exhaustive check of div_by against the IEEE divide: x over bit patterns [lo, hi) with both signs
+__global__ __launch_bounds__(256) void k_div_check(float d, float r, uint32_t lo, uint32_t hi,
+                                                   unsigned long long* bad)
+{
+    uint32_t n = 0;
+    for (uint64_t u = (uint64_t)lo + blockIdx.x * 256u + threadIdx.x; u < hi; u += (uint64_t)gridDim.x * 256u) {
+        for (uint32_t sgn = 0; sgn < 2; ++sgn) {
+            const float x = __uint_as_float((uint32_t)u | (sgn << 31));
+            const float a = div_by(x, d, r), b = x / d;
+            if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) n++;
+        }
+    }
+    wave_count(bad, n);
+}
+void launch_div_check(float d, float r, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_div_check, dim3(8192), dim3(256), 0, st, d, r, lo, hi, bad);
 }
 
 __global__ __launch_bounds__(256) void k_f16(const float* in, uint32_t n, uint16_t* out)

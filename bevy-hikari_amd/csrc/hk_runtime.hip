@@ -253,6 +253,24 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     }
     F.S[0] = c->S[0];
     F.S[1] = c->S[1];
+    F.inv_S[0] = 1.0f / (float)c->S[0];
+    F.inv_S[1] = 1.0f / (float)c->S[1];
+    for (int el = 0; el < 2; ++el) {
+        const uint32_t count = el ? 8u : 16u;
+        const float range = el ? 10.0f : 20.0f;
+        for (uint32_t i = 1u; i <= 16u; ++i) {
+            float py = i <= count ? std::sqrt((float)i / (float)count) * range : 0.0f;
+            float interval = std::fmax(1.0f, py / 5.0f);
+            float q = py / interval;
+            F.sp_py[el][i - 1] = py;
+            F.sp_tap_interval[el][i - 1] = interval;
+            F.sp_tap_count[el][i - 1] = q > 0.0f ? (q >= 4294967296.0f ? 0xFFFFFFFFu : (uint32_t)q) : 0u;
+        }
+    }
+    for (uint32_t tc = 0; tc < 7; ++tc)
+        for (uint32_t j = 0; j < 6; ++j) F.sp_tap_t[tc][j] = (float)j / (float)(tc + 1u);
+    F.inv_s[0] = 1.0f / (float)c->s[0];
+    F.inv_s[1] = 1.0f / (float)c->s[1];
     F.s[0] = c->s[0];
     F.s[1] = c->s[1];
     F.S_row0 = c->S_row0;
@@ -967,6 +985,27 @@ int hk_selftest_f16(hk_ctx* c, const float* in, uint32_t n, uint16_t* out)
     HK_HIP(c, hipStreamSynchronize(st));
     release(d_in);
     release(d_out);
+    return HK_OK;
+}
+
+int hk_selftest_div(hk_ctx* c, float divisor, uint32_t lo, uint32_t hi, uint64_t* mismatches)
+{
+    if (!c || !mismatches || !(divisor > 0.0f)) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, nullptr);
+    unsigned long long* d_bad = nullptr;
+    const size_t bytes = (size_t)COUNTER_SHARDS * COUNTER_STRIDE * 8;
+    HK_HIP(c, hipMalloc(&d_bad, bytes));
+    HK_HIP(c, hipMemsetAsync(d_bad, 0, bytes, st));
+    launch_div_check(divisor, 1.0f / divisor, lo, hi, d_bad, st);
+    HK_HIP(c, hipGetLastError());
+    std::vector<unsigned long long> h(bytes / 8);
+    HK_HIP(c, hipMemcpyAsync(h.data(), d_bad, bytes, hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    release(d_bad);
+    uint64_t total = 0;
+    for (size_t k = 0; k < h.size(); k += COUNTER_STRIDE) total += h[k];
+    *mismatches = total;
     return HK_OK;
 }
 

@@ -160,6 +160,12 @@ class HikariRenderer:
                                           None), "hk_trace")
         return hits
 
+    def selftest_div(self, divisor: float, lo: int, hi: int) -> int:
+        """Mismatches of the kernels' division by a frame dimension against IEEE x / divisor."""
+        n = C.c_uint64()
+        _check(self.ctx, self._L.hk_selftest_div(self.ctx, divisor, lo, hi, C.byref(n)), "hk_selftest_div")
+        return n.value
+
     def selftest_f16(self, values: np.ndarray) -> np.ndarray:
         """The kernels' own f32 -> f16 conversion applied to `values` (uint16 bit patterns)."""
         v = np.ascontiguousarray(values, np.float32)

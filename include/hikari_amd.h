@@ -246,6 +246,9 @@ int hk_trace(hk_ctx* ctx, const float* rays, const float* max_distance, const fl
 /* ---- self-test of the device f16 conversion (pack2x16float, light.wgsl:173-216 pack_reservoir)
  * converts n host floats with the kernels' own conversion; out: n f16 bit patterns (host) */
 int hk_selftest_f16(hk_ctx* ctx, const float* in, uint32_t n, uint16_t* out);
+/* ---- self-test of the kernels' division by a frame dimension (div_by, hk_device.h): counts the
+ * f32 bit patterns x in [lo, hi) (both signs) where div_by(x, divisor) != x / divisor */
+int hk_selftest_div(hk_ctx* ctx, float divisor, uint32_t lo, uint32_t hi, uint64_t* mismatches);
 
 #ifdef __cplusplus
 }

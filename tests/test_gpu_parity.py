@@ -279,3 +279,14 @@ def test_subframe_accumulation_matches_numpy():
     got = r.output(_abi.OUT_ACCUMULATED).view(np.uint16).reshape(h, w, 4)
     want = (acc / np.float32(5.0)).astype(np.float32).astype(np.float16).view(np.uint16)
     assert np.array_equal(got, want)
+
+
+def test_fast_division_by_frame_size_is_exact():
+    """div_by (hk_device.h), the kernels' division by an image dimension, returns the IEEE
+    quotient's bits for every x with |x| in [2^-100, 2^100) (both signs), for every divisor
+    1..4352 (all widths/heights up to 4K plus margin) and the 8K sizes."""
+    from hikari_amd import HikariRenderer
+    r = HikariRenderer(0)
+    lo, hi = 0x0D800000, 0x71800000
+    bad = {d: r.selftest_div(float(d), lo, hi) for d in list(range(1, 4353)) + [7680, 4320, 8192]}
+    assert not any(bad.values()), {d: n for d, n in bad.items() if n}
