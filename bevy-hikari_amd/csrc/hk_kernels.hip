@@ -701,7 +701,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
     const float instance = g1.x;
     const f2 depth_gradient = mk2(g1.y, g1.z);
     f3 sum_irr[C], irradiance[C];
-    float sum_w[C], l0[C], lum_denom[C], m1[C], m2[C], cnt[C];
+    float sum_w[C], l0[C], lum_denom[C], lum_rcp[C], m1[C], m2[C], cnt[C];
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) {
         float variance = D.internal_variance[ch][idx];
@@ -715,6 +715,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         }
         l0[ch] = lum(irradiance[ch]);
         lum_denom[ch] = 4.0f * hk_pow(variance, 0.25f) + 0.001f;
+        lum_rcp[ch] = 1.0f / lum_denom[ch];
         m1[ch] = m2[ch] = cnt[ch] = 0.0f;
     }
 #pragma unroll
@@ -737,7 +738,10 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
             f3 irr = xyz(load_rgba16f(D.internal[ch][LEVEL], sidx));
             if (bad3(irr)) continue;
             float sl = lum(irr);
-            float w_lum = hk_exp((-fabsf(l0[ch] - sl)) / lum_denom[ch]);
+            // x / lum_denom with the per-pixel reciprocal (div_by: the IEEE quotient for normal
+            // results; lum_denom >= 0.001 and |x| <= 2 x 65504 for finite RGBA16F texels, and a
+            // quotient below the normal range rounds exp() to 1 either way)
+            float w_lum = hk_exp(div_by(-fabsf(l0[ch] - sl), lum_denom[ch], lum_rcp[ch]));
             float w = hk_clampf(w_geo * w_lum, 0.0f, 1.0f) * kw;
             sum_irr[ch] = sum_irr[ch] + irr * w;
             sum_w[ch] += w;
