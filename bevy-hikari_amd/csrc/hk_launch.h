@@ -52,6 +52,31 @@ struct ToneArgs {
     uint2* output;
 };
 
+// Dynamic instance update (hk_dynamic.hip): device buffers + scratch, sized by the runtime.
+struct DynamicArgs {
+    hk_instance* instances;
+    uint32_t n_instances;
+    const float* models;       // n x 16, column-major
+    const float* local_aabbs;  // n x 6: local AABB center xyz, half extents xyz (Bevy Aabb)
+    hk_node* tlas;             // 3n - 2 nodes
+    hk_emissive* emissives;
+    uint32_t n_emissives;
+    const hk_material* materials;
+    const hk_primitive* primitives;
+    hk_alias_entry* alias;
+    uint32_t n_alias;
+    hk_node* lbvh;             // 3m - 2 nodes
+    int buckets;
+    // scratch
+    float* areas;              // alias entries
+    void* alias_work;          // 2 x alias entries x 8 B
+    void* boxes;               // max(n, m) x 24 B
+    uint32_t* idx;             // 2 x max(n, m)
+    void* segments;            // 2 x max(n, m) x 12 B
+    uint32_t* flags;           // [0] singular transform, [1] TLAS split levels (G-buffer stack bound)
+};
+void launch_dynamic_update(const DynamicArgs& D, hipStream_t st);
+
 void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, hipStream_t st);
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st);
 void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);

@@ -44,6 +44,9 @@ struct hk_ctx {
     float4* blas_wide = nullptr;  // G-buffer traversal layout (k_build_wide)
     float4* tlas_wide = nullptr;
     uint32_t gb_stack_need = 0;   // TLAS + BLAS subtree depth bound of closest_hit_ordered
+    uint32_t gb_blas_depth = 0;   // BLAS part of it (the TLAS part changes with hk_update_instances)
+    void* dyn_scratch = nullptr;  // hk_update_instances scratch (sized at upload)
+    size_t dyn_bytes = 0;
     bool has_scene = false;
     uchar4* noise = nullptr;
     bool has_noise = false;
@@ -363,6 +366,7 @@ void hk_destroy(hk_ctx* c)
     for (int i = 0; i < 9; ++i) release(c->buf[i]);
     release(c->blas_wide);
     release(c->tlas_wide);
+    release(c->dyn_scratch);
     release(c->tex_desc);
     release(c->texels);
     release(c->tex_lut);
@@ -438,6 +442,9 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
         blas_depth = dd > blas_depth ? dd : blas_depth;
     }
     c->gb_stack_need = depth(tlas, n_tlas) + blas_depth;
+    c->gb_blas_depth = blas_depth;
+    release(c->dyn_scratch);
+    c->dyn_bytes = 0;
     uint32_t* d_aux = nullptr;
     HK_HIP(c, hipMalloc(&d_aux, (size_t)(n_blas ? n_blas : 1) * 12));
     if (n_blas) {
@@ -459,6 +466,88 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
     HK_HIP(c, hipStreamSynchronize(c->stream));
     release(d_aux);
     c->has_scene = true;
+    return HK_OK;
+}
+
+int hk_update_instances(hk_ctx* c, const float* models, const float* local_aabbs, uint32_t count, void* stream)
+{
+    if (!c || !models || !local_aabbs) return HK_ERR_INVALID;
+    if (!c->has_scene) return fail(c, HK_ERR_STATE, "no scene uploaded (hk_scene_upload)");
+    if (count != c->count[4]) return fail(c, HK_ERR_INVALID, "hk_update_instances needs every instance, in upload order");
+    if (c->count[5] != 3u * count - 2u || (c->count[8] && c->count[7] != 3u * c->count[8] - 2u))
+        return fail(c, HK_ERR_STATE, "scene BVHs are not bvh-0.7.1 flattened (3n - 2 nodes); cannot rebuild");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    const uint32_t n = count, m = c->count[8], n_alias = c->count[3];
+    const uint32_t nm = n > m ? n : m;
+    auto align = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t sz[] = {align((size_t)n * 64), align((size_t)n * 24), align((size_t)(n_alias ? n_alias : 1) * 4),
+                         align((size_t)(n_alias ? n_alias : 1) * 16), align((size_t)nm * 24), align((size_t)nm * 8),
+                         align((size_t)nm * 24), align((size_t)3 * n * 4), align(16)};
+    size_t total = 0;
+    for (size_t b : sz) total += b;
+    if (c->dyn_bytes < total) {
+        release(c->dyn_scratch);
+        HK_HIP(c, hipMalloc(&c->dyn_scratch, total));
+        c->dyn_bytes = total;
+    }
+    char* p = (char*)c->dyn_scratch;
+    char* part[9];
+    for (int k = 0; k < 9; ++k) {
+        part[k] = p;
+        p += sz[k];
+    }
+    HK_HIP(c, hipMemcpyAsync(part[0], models, (size_t)n * 64, hipMemcpyHostToDevice, st));
+    HK_HIP(c, hipMemcpyAsync(part[1], local_aabbs, (size_t)n * 24, hipMemcpyHostToDevice, st));
+    HK_HIP(c, hipMemsetAsync(part[8], 0, 16, st));
+    DynamicArgs D;
+    D.instances = (hk_instance*)c->buf[4];
+    D.n_instances = n;
+    D.models = (const float*)part[0];
+    D.local_aabbs = (const float*)part[1];
+    D.tlas = (hk_node*)c->buf[5];
+    D.emissives = (hk_emissive*)c->buf[8];
+    D.n_emissives = m;
+    D.materials = (const hk_material*)c->buf[6];
+    D.primitives = (const hk_primitive*)c->buf[1];
+    D.alias = (hk_alias_entry*)c->buf[3];
+    D.n_alias = n_alias;
+    D.lbvh = (hk_node*)c->buf[7];
+    D.buckets = 6;  // bvh 0.7.1 NUM_BUCKETS (hks_build default)
+    D.areas = (float*)part[2];
+    D.alias_work = part[3];
+    D.boxes = part[4];
+    D.idx = (uint32_t*)part[5];
+    D.segments = part[6];
+    D.flags = (uint32_t*)part[8];
+    timed(c, "update_instances", st, [&] {
+        launch_dynamic_update(D, st);
+        // device-only derivatives of the TLAS: leaf boxes and the G-buffer wide layout
+        launch_fill_leaves(nullptr, 0, nullptr, nullptr, (hk_node*)c->buf[5], c->count[5], (const hk_instance*)c->buf[4],
+                           n, st);
+        launch_build_wide((const hk_node*)c->buf[5], c->count[5], nullptr, nullptr, c->tlas_wide, st);
+    });
+    HK_HIP(c, hipGetLastError());
+    uint32_t flags[2] = {0, 0};
+    HK_HIP(c, hipMemcpyAsync(flags, part[8], 8, hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    if (flags[0]) return fail(c, HK_ERR_INVALID, "singular instance transform");
+    c->gb_stack_need = flags[1] + c->gb_blas_depth;
+    return HK_OK;
+}
+
+int hk_read_scene_array(hk_ctx* c, int array, void* dst, size_t bytes)
+{
+    if (!c || !dst || array < 0 || array > 8) return HK_ERR_INVALID;
+    if (!c->has_scene) return fail(c, HK_ERR_STATE, "no scene uploaded (hk_scene_upload)");
+    const size_t elem[9] = {sizeof(hk_vertex), sizeof(hk_primitive), sizeof(hk_node), sizeof(hk_alias_entry),
+                            sizeof(hk_instance), sizeof(hk_node), sizeof(hk_material), sizeof(hk_node),
+                            sizeof(hk_emissive)};
+    const size_t have = (size_t)c->count[array] * elem[array];
+    if (bytes < have) return fail(c, HK_ERR_INVALID, "destination too small");
+    (void)hipSetDevice(c->device);
+    HK_HIP(c, hipStreamSynchronize(c->stream));
+    if (have) HK_HIP(c, hipMemcpy(dst, c->buf[array], have, hipMemcpyDeviceToHost));
     return HK_OK;
 }
 

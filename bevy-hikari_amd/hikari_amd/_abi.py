@@ -142,6 +142,8 @@ def lib() -> C.CDLL:
         "hk_denoise": (i32, [vp, C.POINTER(hk_settings), C.POINTER(hk_frame_inputs), vp]),
         "hk_tone_sum": (i32, [vp, C.POINTER(hk_settings), vp]),
         "hk_accumulate": (i32, [vp, i32, vp]),
+        "hk_update_instances": (i32, [vp, vp, vp, u32, vp]),
+        "hk_read_scene_array": (i32, [vp, i32, vp, C.c_size_t]),
         "hk_resolve_accumulation": (i32, [vp, vp]),
         "hk_output_info": (i32, [vp, i32, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]),
         "hk_get_output": (i32, [vp, i32, vp, C.c_size_t, i32, vp]),
@@ -176,7 +178,7 @@ def lib() -> C.CDLL:
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
     "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
-    "hk_denoise", "hk_tone_sum", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
+    "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
     "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",
     "hks_add_instance", "hks_build", "hks_get_desc",

@@ -93,6 +93,24 @@ class HikariRenderer:
     def tone_sum(self, settings: _abi.hk_settings, stream=None) -> None:
         _check(self.ctx, self._L.hk_tone_sum(self.ctx, C.byref(settings), stream), "hk_tone_sum")
 
+    def update_instances(self, models: np.ndarray, local_aabbs: np.ndarray, stream=None) -> None:
+        """New transforms of every instance (hk_update_instances): (n, 16) column-major models and
+        (n, 6) local AABBs (center, half extents); the GPU rebuilds instances, TLAS, emissives and
+        the light BVH."""
+        m = np.ascontiguousarray(models, np.float32).reshape(-1, 16)
+        a = np.ascontiguousarray(local_aabbs, np.float32).reshape(-1, 6)
+        if len(m) != len(a):
+            raise ValueError("models and local_aabbs differ in length")
+        _check(self.ctx, self._L.hk_update_instances(self.ctx, m.ctypes.data, a.ctypes.data, len(m), stream),
+               "hk_update_instances")
+
+    def scene_array(self, array: int, dtype, count: int) -> np.ndarray:
+        """Device copy of group-2 scene array `array` (hk_scene_desc order) as `count` records."""
+        out = np.empty(count, dtype)
+        _check(self.ctx, self._L.hk_read_scene_array(self.ctx, array, out.ctypes.data, out.nbytes),
+               "hk_read_scene_array")
+        return out
+
     def accumulate(self, reset: bool = False, stream=None) -> None:
         """Add the tone-mapped output to the sub-frame accumulator (hk_accumulate)."""
         _check(self.ctx, self._L.hk_accumulate(self.ctx, int(reset), stream), "hk_accumulate")

@@ -341,6 +341,23 @@ class Scene:
         self.desc = d
         return d
 
+    def instance_models(self) -> np.ndarray:
+        """(n, 16) float32 column-major model matrices of the instances, in upload order."""
+        return np.stack([col_major(m) for _, _, m in self.instances]).astype(np.float32)
+
+    def instance_local_aabbs(self) -> np.ndarray:
+        """(n, 6) float32 Bevy `Aabb` of each instance's mesh (center xyz, half extents xyz),
+        from the mesh's vertex bounds with the builder's float operations."""
+        out = np.empty((len(self.instances), 6), np.float32)
+        cache = {}
+        for i, (mesh, _, _) in enumerate(self.instances):
+            if mesh not in cache:
+                p = np.asarray(self.meshes[mesh].positions, np.float32)
+                mn, mx = p.min(axis=0), p.max(axis=0)
+                cache[mesh] = np.concatenate([(mn + mx) * np.float32(0.5), (mx - mn) * np.float32(0.5)])
+            out[i] = cache[mesh]
+        return out
+
     def arrays(self) -> dict:
         """numpy views (copies) of the built std430 buffers."""
         assert self.desc is not None

@@ -172,6 +172,18 @@ void hk_settings_default(hk_settings* out);
 int hk_scene_upload(hk_ctx* ctx, const hk_scene_desc* scene);
 int hk_set_noise(hk_ctx* ctx, const uint8_t* rgba8, uint32_t count, uint32_t size);
 
+/* Dynamic instances: `prepare_instances` (instance.rs:284-437) re-run ON THE GPU when
+ * transforms change — instance records (world AABB from the 8 transformed corners of the local AABB,
+ * inverse-transpose model), the TLAS (bvh 0.7.1 binned SAH, 6 buckets, rebuilt, not refitted),
+ * emissive records with their alias tables, and the light BVH; bit-identical to a host rebuild
+ * (hikari_scene.h hks_build) with the same transforms.  models: count x 16 floats
+ * (GlobalTransform::compute_matrix, column-major); local_aabbs: count x 6 floats (the entity's
+ * Bevy `Aabb`: center xyz, half_extents xyz).  count must equal the uploaded instance count
+ * (same order, meshes and materials).  Waits for the stream once (singular-matrix check). */
+int hk_update_instances(hk_ctx* ctx, const float* models, const float* local_aabbs, uint32_t count, void* stream);
+/* copy group-2 scene array `array` (0..8, hk_scene_desc order) back from the device (test/debug) */
+int hk_read_scene_array(hk_ctx* ctx, int array, void* dst, size_t bytes);
+
 /* Sub-frame accumulation (N integrator sub-frames per displayed frame, each
  * exactly one reference frame): hk_accumulate adds the current tone-mapped output (HK_OUT_TONE_MAPPED)
  * to an f32 RGBA accumulator, restarting it when reset != 0; hk_resolve_accumulation writes
