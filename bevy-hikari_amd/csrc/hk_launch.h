@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "hk_device.h"
+#include "../../include/hk_post.h"
 
 namespace hk {
 
@@ -76,6 +77,15 @@ struct DynamicArgs {
     uint32_t* flags;           // [0] singular transform, [1] TLAS split levels (G-buffer stack bound)
 };
 void launch_dynamic_update(const DynamicArgs& D, hipStream_t st);
+
+// Post-process (hk_post.hip over include/hk_post.h)
+struct PostArgs {
+    hk_pp_frame frame;
+    hk_pp_inputs in;
+};
+void launch_smaa(const PostArgs& P, hipStream_t st);
+void launch_smaa_extrapolate(const PostArgs& P, hipStream_t st);
+void launch_taa(const PostArgs& P, hipStream_t st);
 
 void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, hipStream_t st);
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st);

@@ -70,6 +70,9 @@ struct hk_ctx {
     float2* g_depth_gradient = nullptr;
     float2* g_instance_material = nullptr;
     float4* g_velocity_uv = nullptr;
+    float4* g_prev_position = nullptr;    // the previous frame's planes (prepass.rs:309-317 swap)
+    float4* g_prev_velocity_uv = nullptr;
+    uint32_t head = 0;                    // frame_number % 2 (PostProcessTextures.head)
     // light targets
     uint2* albedo = nullptr;
     float* variance[3] = {};
@@ -82,7 +85,10 @@ struct hk_ctx {
     float4* geom = nullptr;
     int last_denoised_channels = 3;
     uint2* denoised[3] = {};
-    uint2* tone = nullptr;
+    uint2* tone_buf[2] = {};      // tone_mapping_output[2], written at [head]
+    uint2* upscale = nullptr;     // upscale_output[0] (SMAA TU4x), U = ceil(S * 2 / ratio)
+    uint2* taa_buf[2] = {};       // taa_output[2]
+    uint32_t upscale_wh[2] = {0, 0}, taa_wh[2] = {0, 0};
     float4* accum = nullptr;      // sub-frame accumulator (hk_accumulate), allocated on first use
     uint2* accum_out = nullptr;
     uint32_t accum_n = 0;
@@ -141,7 +147,14 @@ void free_targets(hk_ctx* c)
         release(c->internal_variance[ch]);
     }
     release(c->geom);
-    release(c->tone);
+    for (int k = 0; k < 2; ++k) {
+        release(c->tone_buf[k]);
+        release(c->taa_buf[k]);
+    }
+    release(c->upscale);
+    release(c->g_prev_position);
+    release(c->g_prev_velocity_uv);
+    c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
     release(c->accum);
     release(c->accum_out);
     c->accum_n = 0;
@@ -334,6 +347,7 @@ void hk_settings_default(hk_settings* o)
     o->denoise = 1;
     o->taa = 0;
     o->upscale_ratio = 2.0f;
+    o->upscale = 0;
 }
 
 int hk_create(int device, hk_ctx** out)
@@ -642,6 +656,10 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
     HK_HIP(c, hipMalloc(&c->g_depth_gradient, SP * sizeof(float2)));
     HK_HIP(c, hipMalloc(&c->g_instance_material, SP * sizeof(float2)));
     HK_HIP(c, hipMalloc(&c->g_velocity_uv, SP * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->g_prev_position, SP * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->g_prev_velocity_uv, SP * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->g_prev_position, 0, SP * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->g_prev_velocity_uv, 0, SP * sizeof(float4)));
     HK_HIP(c, hipMalloc(&c->albedo, SP * sizeof(uint2)));
     HK_HIP(c, hipMemset(c->g_position, 0, SP * sizeof(float4)));
     HK_HIP(c, hipMemset(c->g_normal, 0, SP * sizeof(uint32_t)));
@@ -672,8 +690,10 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
     }
     HK_HIP(c, hipMalloc(&c->geom, 2 * sp * sizeof(float4)));
     HK_HIP(c, hipMemset(c->geom, 0, 2 * sp * sizeof(float4)));
-    HK_HIP(c, hipMalloc(&c->tone, sp * sizeof(uint2)));
-    HK_HIP(c, hipMemset(c->tone, 0, sp * sizeof(uint2)));
+    for (int k = 0; k < 2; ++k) {
+        HK_HIP(c, hipMalloc(&c->tone_buf[k], sp * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->tone_buf[k], 0, sp * sizeof(uint2)));
+    }
     HK_HIP(c, hipDeviceSynchronize());
     c->sized = true;
     return HK_OK;
@@ -705,6 +725,10 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         return fail(c, HK_ERR_INVALID, "scene BVH too deep for the G-buffer traversal stack (TLAS + BLAS depth > 64)");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    // a new frame: this frame's planes replace the previous ones (prepass.rs:309-317)
+    std::swap(c->g_position, c->g_prev_position);
+    std::swap(c->g_velocity_uv, c->g_prev_velocity_uv);
+    c->head = in->frame_number & 1u;
     FrameArgs A = frame_args(c, nullptr, in);
     ViewArgs V;
     for (int i = 0; i < 3; ++i) V.world_position[i] = in->view.world_position[i];
@@ -731,6 +755,14 @@ int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, i
     default: return fail(c, HK_ERR_INVALID, "unknown G-buffer plane");
     }
     if (bytes != need) return fail(c, HK_ERR_INVALID, "G-buffer plane size mismatch");
+    // a new frame's position / velocity plane: the current one becomes the previous (prepass.rs:309-317)
+    if (plane == 0) {
+        std::swap(c->g_position, c->g_prev_position);
+        dst = c->g_position;
+    } else if (plane == 4) {
+        std::swap(c->g_velocity_uv, c->g_prev_velocity_uv);
+        dst = c->g_velocity_uv;
+    }
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
     HK_HIP(c, hipMemcpyAsync(dst, data, bytes, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
@@ -762,6 +794,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    c->head = in->frame_number & 1u;
     FrameArgs A = frame_args(c, settings, in);
     timed(c, "full_screen_albedo", st, [&] { launch_albedo(A, c->albedo, st); });
     ChannelArgs C0 = channel(c, A.F.number, 0);
@@ -820,8 +853,72 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     T.direct = settings->denoise ? c->denoised[0] : c->render[0];
     T.emissive = settings->denoise ? c->denoised[1] : c->render[1];
     T.indirect = settings->indirect_bounces == 0u ? nullptr : (settings->denoise ? c->denoised[2] : c->render[2]);
-    T.output = c->tone;
+    T.output = c->tone_buf[c->head];
     timed(c, "tone_mapping", st, [&] { launch_tone(A, T, st); });
+    HK_HIP(c, hipGetLastError());
+    return HK_OK;
+}
+
+int hk_post_process(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in, void* stream)
+{
+    int rc = check_ready(c, false);
+    if (rc) return rc;
+    if (!st || !in) return fail(c, HK_ERR_INVALID, "null settings or frame inputs");
+    if (c->S_rows != (int32_t)c->S[1]) return fail(c, HK_ERR_STATE, "hk_post_process needs a whole-frame context");
+    (void)hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    c->head = in->frame_number & 1u;
+    const uint32_t head = c->head;
+    // post_process.rs:663-731 sizes: ceil(S * scale), scale = 1 / ratio, x 2 after SMAA TU4x
+    float scale = 1.0f / c->ratio;
+    const bool smaa = st->upscale == 0u, taa = st->taa == 0u;
+    PostArgs P;
+    P.frame.number = in->frame_number;
+    for (int k = 0; k < 4; ++k) P.frame.clear_color[k] = st->clear_color[k];
+    P.frame.upscale_ratio = c->ratio;
+    auto tex = [](const void* d, uint32_t w, uint32_t h, uint32_t f16, uint32_t comps) {
+        hk_pp_tex t;
+        t.data = d, t.w = w, t.h = h, t.f16 = f16, t.comps = comps;
+        return t;
+    };
+    const uint32_t S0 = c->S[0], S1 = c->S[1];
+    P.in.position = tex(c->g_position, S0, S1, 0, 4);
+    P.in.previous_position = tex(c->g_prev_position, S0, S1, 0, 4);
+    P.in.velocity_uv = tex(c->g_velocity_uv, S0, S1, 0, 4);
+    P.in.previous_velocity_uv = tex(c->g_prev_velocity_uv, S0, S1, 0, 4);
+    P.in.instance_material = tex(c->g_instance_material, S0, S1, 0, 2);
+    hk_pp_tex taa_input = tex(c->tone_buf[head], c->s[0], c->s[1], 1, 4);
+    if (smaa) {
+        scale *= 2.0f;
+        const uint32_t U0 = (uint32_t)std::ceil((float)S0 * scale), U1 = (uint32_t)std::ceil((float)S1 * scale);
+        if (!c->upscale || c->upscale_wh[0] != U0 || c->upscale_wh[1] != U1) {
+            release(c->upscale);
+            HK_HIP(c, hipMalloc(&c->upscale, (size_t)U0 * U1 * sizeof(uint2)));
+            HK_HIP(c, hipMemset(c->upscale, 0, (size_t)U0 * U1 * sizeof(uint2)));
+            c->upscale_wh[0] = U0, c->upscale_wh[1] = U1;
+        }
+        P.in.render = tex(c->tone_buf[head], c->s[0], c->s[1], 1, 4);
+        P.in.previous_render = tex(c->tone_buf[1u - head], c->s[0], c->s[1], 1, 4);
+        P.in.output = hk_pp_out{(uint16_t*)c->upscale, U0, U1};
+        timed(c, "smaa_tu4x", s, [&] { launch_smaa(P, s); });
+        timed(c, "smaa_tu4x_extrapolate", s, [&] { launch_smaa_extrapolate(P, s); });
+        taa_input = tex(c->upscale, U0, U1, 1, 4);
+    }
+    if (taa) {
+        const uint32_t T0 = (uint32_t)std::ceil((float)S0 * scale), T1 = (uint32_t)std::ceil((float)S1 * scale);
+        if (!c->taa_buf[0] || c->taa_wh[0] != T0 || c->taa_wh[1] != T1) {
+            for (int k = 0; k < 2; ++k) {
+                release(c->taa_buf[k]);
+                HK_HIP(c, hipMalloc(&c->taa_buf[k], (size_t)T0 * T1 * sizeof(uint2)));
+                HK_HIP(c, hipMemset(c->taa_buf[k], 0, (size_t)T0 * T1 * sizeof(uint2)));
+            }
+            c->taa_wh[0] = T0, c->taa_wh[1] = T1;
+        }
+        P.in.render = taa_input;
+        P.in.previous_render = tex(c->taa_buf[1u - head], T0, T1, 1, 4);
+        P.in.output = hk_pp_out{(uint16_t*)c->taa_buf[head], T0, T1};
+        timed(c, "taa_jasmine", s, [&] { launch_taa(P, s); });
+    }
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -840,7 +937,7 @@ int hk_accumulate(hk_ctx* c, int reset, void* stream)
         reset = 1;
     }
     if (reset) c->accum_n = 0;
-    timed(c, "accumulate", st, [&] { launch_accumulate(c->tone, c->accum, (uint32_t)n, reset, st); });
+    timed(c, "accumulate", st, [&] { launch_accumulate(c->tone_buf[c->head], c->accum, (uint32_t)n, reset, st); });
     HK_HIP(c, hipGetLastError());
     c->accum_n += 1;
     return HK_OK;
@@ -871,7 +968,9 @@ static void* output_ptr(hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* b
         p = c->render[id - HK_OUT_RENDER_DIRECT]; break;
     case HK_OUT_DENOISED_DIRECT: case HK_OUT_DENOISED_EMISSIVE: case HK_OUT_DENOISED_INDIRECT:
         p = c->denoised[id - HK_OUT_DENOISED_DIRECT]; break;
-    case HK_OUT_TONE_MAPPED: p = c->tone; break;
+    case HK_OUT_TONE_MAPPED: p = c->tone_buf[c->head]; break;
+    case HK_OUT_UPSCALED: p = c->upscale; W = c->upscale_wh[0]; H = c->upscale_wh[1]; break;
+    case HK_OUT_TAA: p = c->taa_buf[c->head]; W = c->taa_wh[0]; H = c->taa_wh[1]; break;
     case HK_OUT_ACCUMULATED: p = c->accum_out; break;
     case HK_OUT_GBUF_POSITION: p = c->g_position; W = c->S[0]; H = (uint32_t)c->S_rows; B = 16; break;
     case HK_OUT_GBUF_NORMAL: p = c->g_normal; W = c->S[0]; H = (uint32_t)c->S_rows; B = 4; break;

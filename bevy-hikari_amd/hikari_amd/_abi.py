@@ -30,6 +30,8 @@ OUT_GBUF_DEPTH_GRADIENT = 13
 OUT_GBUF_INSTANCE_MATERIAL = 14
 OUT_GBUF_VELOCITY_UV = 15
 OUT_ACCUMULATED = 17
+OUT_UPSCALED = 18
+OUT_TAA = 19
 OUT_DENOISE_INTERNAL_VARIANCE = 16
 RESERVOIR_BUFFERS = 10
 
@@ -71,6 +73,7 @@ class hk_settings(C.Structure):
         ("denoise", C.c_uint32),
         ("taa", C.c_uint32),
         ("upscale_ratio", C.c_float),
+        ("upscale", C.c_uint32),
     ]
 
 
@@ -142,6 +145,7 @@ def lib() -> C.CDLL:
         "hk_denoise": (i32, [vp, C.POINTER(hk_settings), C.POINTER(hk_frame_inputs), vp]),
         "hk_tone_sum": (i32, [vp, C.POINTER(hk_settings), vp]),
         "hk_accumulate": (i32, [vp, i32, vp]),
+        "hk_post_process": (i32, [vp, C.POINTER(hk_settings), C.POINTER(hk_frame_inputs), vp]),
         "hk_update_instances": (i32, [vp, vp, vp, u32, vp]),
         "hk_read_scene_array": (i32, [vp, i32, vp, C.c_size_t]),
         "hk_resolve_accumulation": (i32, [vp, vp]),
@@ -178,7 +182,7 @@ def lib() -> C.CDLL:
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
     "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
-    "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
+    "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
     "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",
     "hks_add_instance", "hks_build", "hks_get_desc",

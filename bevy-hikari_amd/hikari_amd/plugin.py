@@ -111,6 +111,11 @@ class HikariRenderer:
                "hk_read_scene_array")
         return out
 
+    def post_process(self, settings: _abi.hk_settings, inputs: _abi.hk_frame_inputs, stream=None) -> None:
+        """SMAA TU4x + TAA Jasmine after tone mapping (hk_post_process)."""
+        _check(self.ctx, self._L.hk_post_process(self.ctx, C.byref(settings), C.byref(inputs), stream),
+               "hk_post_process")
+
     def accumulate(self, reset: bool = False, stream=None) -> None:
         """Add the tone-mapped output to the sub-frame accumulator (hk_accumulate)."""
         _check(self.ctx, self._L.hk_accumulate(self.ctx, int(reset), stream), "hk_accumulate")

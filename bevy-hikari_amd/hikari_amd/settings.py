@@ -89,6 +89,7 @@ class HikariSettings:
         s.denoise = int(bool(self.denoise))
         s.taa = self.taa.value
         s.upscale_ratio = float(self.upscale.ratio())
+        s.upscale = 0 if self.upscale.kind == "SmaaTu4x" else 1
         return s
 
 

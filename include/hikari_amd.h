@@ -98,8 +98,9 @@ typedef struct hk_settings {
     uint32_t emissive_spatial_reuse;
     uint32_t indirect_spatial_reuse;
     uint32_t denoise;
-    uint32_t taa;           /* 0 = Jasmine, 1 = None (post-path, not run here) */
+    uint32_t taa;           /* 0 = Jasmine, 1 = None (hk_post_process) */
     float upscale_ratio;    /* Upscale::ratio(), clamped to [1, 2] (lib.rs:501-505) */
+    uint32_t upscale;       /* 0 = SmaaTu4x (default), 1 = Fsr1 (not provided: hk_post_process skips it) */
 } hk_settings;
 
 /* The parts of Bevy's `View` uniform the integrator reads (light.wgsl:714-727). */
@@ -147,7 +148,9 @@ typedef enum hk_output_id {
     HK_OUT_GBUF_VELOCITY_UV = 15, /* float4, S */
     HK_OUT_DENOISE_INTERNAL_VARIANCE = 16, /* R32F, s (last channel denoised) */
     HK_OUT_ACCUMULATED = 17,      /* RGBA16F, s: hk_resolve_accumulation */
-    HK_OUT_COUNT = 18
+    HK_OUT_UPSCALED = 18,         /* RGBA16F, ceil(S * 2 / ratio): SMAA TU4x output (upscale_output[0]) */
+    HK_OUT_TAA = 19,              /* RGBA16F: TAA Jasmine output of this frame (taa_output[head]) */
+    HK_OUT_COUNT = 20
 } hk_output_id;
 
 /* Reservoir buffer ids 0..9 as allocated by light.rs:350-361; the channel pairs
@@ -183,6 +186,13 @@ int hk_set_noise(hk_ctx* ctx, const uint8_t* rgba8, uint32_t count, uint32_t siz
 int hk_update_instances(hk_ctx* ctx, const float* models, const float* local_aabbs, uint32_t count, void* stream);
 /* copy group-2 scene array `array` (0..8, hk_scene_desc order) back from the device (test/debug) */
 int hk_read_scene_array(hk_ctx* ctx, int array, void* dst, size_t bytes);
+
+/* Post-process after tone mapping (post_process.rs:1236-1276): SMAA TU4x temporal 2x upsampling
+ * (smaa.wgsl `smaa_tu4x` + `smaa_tu4x_extrapolate`, when settings->upscale == 0) then TAA Jasmine
+ * (taa.wgsl, when settings->taa == 0).  Reads the previous frame's tone-mapped output and G-buffer
+ * position / velocity planes (the reference's ping-pong textures, prepass.rs:309-317, head =
+ * frame_number % 2).  Whole-frame contexts only. */
+int hk_post_process(hk_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs, void* stream);
 
 /* Sub-frame accumulation (N integrator sub-frames per displayed frame, each
  * exactly one reference frame): hk_accumulate adds the current tone-mapped output (HK_OUT_TONE_MAPPED)

@@ -22,6 +22,7 @@
 #include "hk_oracle.h"
 #include "../include/hk_math.h"
 #include "../include/hk_texture.h"
+#include "../include/hk_post.h"
 
 #include <stdlib.h>
 #include <stdio.h>
@@ -139,6 +140,9 @@ struct hko_ctx {
     float* g_depth_gradient;  /* 2 */
     float* g_instance_material; /* 2 */
     float* g_velocity_uv;     /* 4 */
+    float* g_prev_position;   /* previous frame's planes (prepass.rs:309-317 swap) */
+    float* g_prev_velocity_uv;
+    uint32_t head;            /* frame_number % 2 */
     /* light textures */
     uint16_t* albedo;         /* 4 x f16, S */
     float* variance[3];       /* s */
@@ -148,7 +152,10 @@ struct hko_ctx {
     uint16_t* internal[4];
     float* internal_variance;
     uint16_t* denoised[3];
-    uint16_t* tone;
+    uint16_t* tone;           /* = tone_buf[head] */
+    uint16_t* tone_buf[2];
+    uint16_t* upscale; uint32_t upscale_wh[2];
+    uint16_t* taa_buf[2]; uint32_t taa_wh[2];
     hk_counters counters;
     int32_t band_y0, band_y1; /* rows computed by every pass (whole frame by default) */
 };
@@ -1812,6 +1819,8 @@ hko_ctx* hko_create(const hk_scene_desc* sc, const uint8_t* noise, uint32_t widt
     c->g_depth_gradient = (float*)calloc(S * 2, sizeof(float));
     c->g_instance_material = (float*)calloc(S * 2, sizeof(float));
     c->g_velocity_uv = (float*)calloc(S * 4, sizeof(float));
+    c->g_prev_position = (float*)calloc(S * 4, sizeof(float));
+    c->g_prev_velocity_uv = (float*)calloc(S * 4, sizeof(float));
     c->albedo = (uint16_t*)calloc(S * 4, sizeof(uint16_t));
     for (int i = 0; i < 3; ++i) {
         c->variance[i] = (float*)calloc(s, sizeof(float));
@@ -1821,7 +1830,9 @@ hko_ctx* hko_create(const hk_scene_desc* sc, const uint8_t* noise, uint32_t widt
     for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) c->reservoirs[i] = (hk_packed_reservoir*)calloc(S, sizeof(hk_packed_reservoir));
     for (int i = 0; i < 4; ++i) c->internal[i] = (uint16_t*)calloc(s * 4, sizeof(uint16_t));
     c->internal_variance = (float*)calloc(s, sizeof(float));
-    c->tone = (uint16_t*)calloc(s * 4, sizeof(uint16_t));
+    c->tone_buf[0] = (uint16_t*)calloc(s * 4, sizeof(uint16_t));
+    c->tone_buf[1] = (uint16_t*)calloc(s * 4, sizeof(uint16_t));
+    c->tone = c->tone_buf[0];
     return c;
 }
 
@@ -1862,7 +1873,9 @@ void hko_destroy(hko_ctx* c)
     for (int i = 0; i < 3; ++i) { free(c->variance[i]); free(c->render[i]); free(c->denoised[i]); }
     for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) free(c->reservoirs[i]);
     for (int i = 0; i < 4; ++i) free(c->internal[i]);
-    free(c->internal_variance); free(c->tone);
+    free(c->internal_variance); free(c->tone_buf[0]); free(c->tone_buf[1]);
+    free(c->g_prev_position); free(c->g_prev_velocity_uv);
+    free(c->upscale); free(c->taa_buf[0]); free(c->taa_buf[1]);
     free(c);
 }
 
@@ -1881,8 +1894,22 @@ static void add_counts(hko_ctx* c, const Counts* k)
 static int omp_get_max_threads(void) { return 1; }
 #endif
 
+static void set_head(hko_ctx* c, uint32_t frame_number)
+{
+    c->head = frame_number & 1u;
+    c->tone = c->tone_buf[c->head];
+}
+
 void hko_render_gbuffer(hko_ctx* c, const hk_frame_inputs* in)
 {
+    /* a new frame: this frame's planes replace the previous ones (prepass.rs:309-317) */
+    float* t = c->g_position;
+    c->g_position = c->g_prev_position;
+    c->g_prev_position = t;
+    t = c->g_velocity_uv;
+    c->g_velocity_uv = c->g_prev_velocity_uv;
+    c->g_prev_velocity_uv = t;
+    set_head(c, in->frame_number);
 #pragma omp parallel HKO_THREADS(c)
     {
         Counts k = {0, 0, 0};
@@ -1914,6 +1941,7 @@ static void run_pass(hko_ctx* c, const Pass* P, Kind kind)
 /* LightNode::run (light.rs:590-702) */
 void hko_render_frame(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
 {
+    set_head(c, in->frame_number);
     Pass P;
     memset(&P, 0, sizeof(P));
     P.c = c;
@@ -2006,6 +2034,67 @@ void hko_tone_sum(hko_ctx* c, const hk_settings* st)
     }
 }
 
+/* post_process.rs:1236-1276: SMAA TU4x then TAA Jasmine (include/hk_post.h, shared with the GPU) */
+static hk_pp_tex pp_tex(const void* d, uint32_t w, uint32_t h, uint32_t f16, uint32_t comps)
+{
+    hk_pp_tex t;
+    t.data = d, t.w = w, t.h = h, t.f16 = f16, t.comps = comps;
+    return t;
+}
+void hko_post_process(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
+{
+    set_head(c, in->frame_number);
+    const uint32_t head = c->head;
+    float scale = 1.0f / c->ratio;
+    hk_pp_frame F;
+    F.number = in->frame_number;
+    for (int k = 0; k < 4; ++k) F.clear_color[k] = st->clear_color[k];
+    F.upscale_ratio = c->ratio;
+    hk_pp_inputs I;
+    const uint32_t S0 = c->S[0], S1 = c->S[1];
+    I.position = pp_tex(c->g_position, S0, S1, 0, 4);
+    I.previous_position = pp_tex(c->g_prev_position, S0, S1, 0, 4);
+    I.velocity_uv = pp_tex(c->g_velocity_uv, S0, S1, 0, 4);
+    I.previous_velocity_uv = pp_tex(c->g_prev_velocity_uv, S0, S1, 0, 4);
+    I.instance_material = pp_tex(c->g_instance_material, S0, S1, 0, 2);
+    hk_pp_tex taa_input = pp_tex(c->tone_buf[head], c->s[0], c->s[1], 1, 4);
+    if (st->upscale == 0u) {
+        scale *= 2.0f;
+        const uint32_t U0 = (uint32_t)ceilf((float)S0 * scale), U1 = (uint32_t)ceilf((float)S1 * scale);
+        if (!c->upscale || c->upscale_wh[0] != U0 || c->upscale_wh[1] != U1) {
+            free(c->upscale);
+            c->upscale = (uint16_t*)calloc((size_t)U0 * U1 * 4, sizeof(uint16_t));
+            c->upscale_wh[0] = U0, c->upscale_wh[1] = U1;
+        }
+        I.render = pp_tex(c->tone_buf[head], c->s[0], c->s[1], 1, 4);
+        I.previous_render = pp_tex(c->tone_buf[1u - head], c->s[0], c->s[1], 1, 4);
+        I.output.data = c->upscale, I.output.w = U0, I.output.h = U1;
+#pragma omp parallel for schedule(static) HKO_THREADS(c)
+        for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
+            for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) hk_pp_smaa_tu4x(&F, &I, x, y);
+#pragma omp parallel for schedule(static) HKO_THREADS(c)
+        for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
+            for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) hk_pp_smaa_extrapolate(&I.output, x, y);
+        taa_input = pp_tex(c->upscale, U0, U1, 1, 4);
+    }
+    if (st->taa == 0u) {
+        const uint32_t T0 = (uint32_t)ceilf((float)S0 * scale), T1 = (uint32_t)ceilf((float)S1 * scale);
+        if (!c->taa_buf[0] || c->taa_wh[0] != T0 || c->taa_wh[1] != T1) {
+            for (int k = 0; k < 2; ++k) {
+                free(c->taa_buf[k]);
+                c->taa_buf[k] = (uint16_t*)calloc((size_t)T0 * T1 * 4, sizeof(uint16_t));
+            }
+            c->taa_wh[0] = T0, c->taa_wh[1] = T1;
+        }
+        I.render = taa_input;
+        I.previous_render = pp_tex(c->taa_buf[1u - head], T0, T1, 1, 4);
+        I.output.data = c->taa_buf[head], I.output.w = T0, I.output.h = T1;
+#pragma omp parallel for schedule(static) HKO_THREADS(c)
+        for (int32_t y = 0; y < (int32_t)T1; ++y)
+            for (int32_t x = 0; x < (int32_t)T0; ++x) hk_pp_taa(&F, &I, x, y);
+    }
+}
+
 void* hko_output(hko_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* bpp)
 {
     uint32_t W = c->s[0], H = c->s[1], B = 8;
@@ -2019,6 +2108,8 @@ void* hko_output(hko_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* bpp)
     case HK_OUT_DENOISED_DIRECT: case HK_OUT_DENOISED_EMISSIVE: case HK_OUT_DENOISED_INDIRECT:
         p = c->denoised[id - HK_OUT_DENOISED_DIRECT]; break;
     case HK_OUT_TONE_MAPPED: p = c->tone; break;
+    case HK_OUT_UPSCALED: p = c->upscale; W = c->upscale_wh[0]; H = c->upscale_wh[1]; break;
+    case HK_OUT_TAA: p = c->taa_buf[c->head]; W = c->taa_wh[0]; H = c->taa_wh[1]; break;
     case HK_OUT_GBUF_POSITION: p = c->g_position; W = c->S[0]; H = c->S[1]; B = 16; break;
     case HK_OUT_GBUF_NORMAL: p = c->g_normal; W = c->S[0]; H = c->S[1]; B = 4; break;
     case HK_OUT_GBUF_DEPTH_GRADIENT: p = c->g_depth_gradient; W = c->S[0]; H = c->S[1]; B = 8; break;

@@ -32,6 +32,8 @@ typedef struct hko_ctx hko_ctx;
 hko_ctx* hko_create(const hk_scene_desc* scene, const uint8_t* noise, uint32_t width, uint32_t height,
                     float upscale_ratio, int threads);
 void hko_destroy(hko_ctx* ctx);
+/* SMAA TU4x + TAA Jasmine (hk_post_process) */
+void hko_post_process(hko_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs);
 /* material textures (hk_texture_upload) and a direct sampling entry for the KATs */
 int hko_set_textures(hko_ctx* ctx, const hk_texture* textures, uint32_t count);
 void hko_sample_texture(const hko_ctx* ctx, uint32_t id, const float* uv, uint32_t n, float* out);

@@ -55,6 +55,7 @@ def lib() -> C.CDLL:
         "hko_f32_to_f16": (u32, [f]),
         "hko_f32_to_f16_array": (None, [C.c_void_p, C.c_size_t, C.c_void_p]),
         "hko_set_textures": (C.c_int, [vp, vp, u32]),
+        "hko_post_process": (None, [vp, vp, vp]),
         "hko_sample_texture": (None, [vp, u32, vp, u32, vp]),
         "hko_hash": (u32, [u32]),
     }
@@ -103,6 +104,9 @@ class Oracle:
 
     def set_band(self, y0: int, rows: int, halo: int = 40):
         self._L.hko_set_band(self.ctx, y0, rows, halo)
+
+    def post_process(self, settings, inputs):
+        self._L.hko_post_process(self.ctx, C.byref(settings), C.byref(inputs))
 
     def render_gbuffer(self, inputs):
         self._L.hko_render_gbuffer(self.ctx, C.byref(inputs))

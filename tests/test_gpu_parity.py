@@ -364,3 +364,27 @@ def test_gpu_instance_update_matches_host_rebuild(scene_fn):
             x.tone_sum(s)
         _compare_frame(r, o, f, errors)
     assert not errors, "\n".join(errors[:10])
+
+
+@pytest.mark.parametrize("ratio_setting,taa", [("SMAA_TU_2_0", "Jasmine"), ("SMAA_TU_1_0", "Jasmine"),
+                                               ("SMAA_TU_2_0", "None_")])
+def test_post_process_smaa_taa_bit_exact(ratio_setting, taa):
+    """SMAA TU4x + TAA Jasmine (hk_post_process) on the GPU vs the oracle, bit for bit, over
+    frames with both jitter parities (the reference default pipeline is SMAA_TU_2_0 + Jasmine)."""
+    from hikari_amd import HikariSettings, Taa, Upscale, _abi, frame_inputs
+    w, h = 62, 41
+    st = HikariSettings(upscale=getattr(Upscale, ratio_setting), taa=getattr(Taa, taa))
+    scene, cam, lights, r, o = _setup(w, h, st)
+    s = st.to_c()
+    for f in range(4):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+            x.post_process(s, fi)
+        outs = [_abi.OUT_TONE_MAPPED, _abi.OUT_UPSCALED] + ([_abi.OUT_TAA] if taa == "Jasmine" else [])
+        for oid in outs:
+            m = mismatch_report(canon_plane(10, r.output(oid)), canon_plane(10, o.output(oid)), f"frame {f} output {oid}")
+            assert not m, m

@@ -95,3 +95,35 @@ def test_textured_frames_differ_from_untextured_and_are_deterministic():
         outs.append(canon_plane(10, o.output(10)).copy())
     assert np.array_equal(outs[0], outs[1])
     assert not np.array_equal(outs[0], outs[2])
+
+
+def test_oracle_post_process_smaa_current_samples_and_sizes():
+    """SMAA TU4x writes each input texel unchanged at its jittered output position
+    (smaa.wgsl:123-126, 197) and the upscaled / TAA planes have the reference's sizes
+    (post_process.rs:663-731: ceil(S * 2 / ratio))."""
+    import math
+    from hikari_amd import HikariSettings, Upscale, _abi, examples, frame_inputs, load_noise
+    from oracle import Oracle
+    W, H = 33, 21
+    st = HikariSettings(upscale=Upscale.SMAA_TU_2_0)
+    scene, cam, lights = examples.cornell()
+    o = Oracle(scene.build(), load_noise(), W, H, st.upscale.ratio())
+    s = st.to_c()
+    for f in range(3):
+        fi = frame_inputs(f, cam, lights, W, H)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.denoise(s, fi)
+        o.tone_sum(s)
+        o.post_process(s, fi)
+        tone = o.output(_abi.OUT_TONE_MAPPED).view(np.uint16).reshape(math.ceil(H / 2), math.ceil(W / 2), 4)
+        up = o.output(_abi.OUT_UPSCALED).view(np.uint16)
+        taa = o.output(_abi.OUT_TAA).view(np.uint16)
+        assert up.shape[:2] == (H, W) and taa.shape[:2] == (H, W)
+        up = up.reshape(H, W, 4)
+        j = 0 if f % 2 == 0 else 1
+        sub = up[j::2, j::2]
+        hh, ww = sub.shape[:2]
+        assert np.array_equal(sub[..., :3], tone[:hh, :ww, :3])
+        assert np.all(sub[..., 3] == 0x3C00)  # alpha 1.0
+        assert np.isfinite(taa.view(np.float16)).all()
