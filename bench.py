@@ -64,6 +64,9 @@ CONFIGS = {
     # configs[3]
     "city-4k": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True,
                     workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, row bands + RCCL all-gather"),
+    # per-frame fixed cost probe (launch / host overhead floor); not a BASELINE config
+    "cornell-tiny-overhead": dict(scene="cornell", width=64, height=64, spatial=False, denoise=False,
+                                  workload="examples/cornell.rs 64x64 (host/launch overhead probe)"),
     # configs[4]: 16 integrator sub-frames (each one reference frame) accumulated per displayed frame,
     # one all-gather per displayed frame
     "city-4k-16spp": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, spp=16,
@@ -139,9 +142,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus and world == 1 and args.gpus != 1:
         print(f"warning: --gpus {args.gpus} without a distributed launcher; running 1 rank", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # HK_BENCH_REHEARSAL=1: rehearse the multi-rank path on ONE GPU (every rank on cuda:0, gloo
+    # collectives through host memory) — a correctness check of the band / gather / reduction
+    # logic, never a measurement.  The real N-GPU run uses RCCL over xGMI.
+    rehearsal = os.environ.get("HK_BENCH_REHEARSAL") == "1"
+    device = 0 if rehearsal else local
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H = cfg["width"], cfg["height"]
     scene, cam, lights = examples.SCENES[cfg["scene"]]()
@@ -152,7 +163,7 @@ def main():
     # row band of this rank (hikari_amd/bands.py)
     b = band_of(rank, world, H)
     band = b.rows
-    r = HikariRenderer(local)
+    r = HikariRenderer(device)
     r.set_noise()
     r.upload_scene(scene)
     r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
@@ -164,8 +175,12 @@ def main():
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
-    band_t = torch.empty((band, W, 4), dtype=torch.float16, device="cuda")
-    full_t = torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") if world > 1 else None
+    # double-buffered band / gathered frame: the all-gather of frame f runs on RCCL's stream
+    # while frame f+1 renders; a buffer is reused only after its previous gather completed
+    band_t = [torch.empty((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
+    full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
+        if world > 1 else None
+    pending = [None, None]
 
     spp = cfg.get("spp", 1)
     shown = hikari_amd._abi.OUT_TONE_MAPPED if spp == 1 else hikari_amd._abi.OUT_ACCUMULATED
@@ -184,12 +199,27 @@ def main():
         if spp > 1:
             r.resolve_accumulation(sp)
         if world > 1:
-            r.copy_output_rows(shown, core0, core_rows, band_t.data_ptr(), False, sp)
-            dist.all_gather_into_tensor(full_t, band_t)
+            k = f & 1
+            if pending[k] is not None:
+                pending[k].wait()  # device-side: the stream waits for that gather
+            r.copy_output_rows(shown, core0, core_rows, band_t[k].data_ptr(), False, sp)
+            if rehearsal:
+                parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
+                dist.all_gather(parts, band_t[k].cpu())
+                full_t[k].copy_(torch.cat(parts))
+            else:
+                pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
+
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
 
     for f in range(args.warmup):
         step(f)
     if world > 1:
+        drain()
         dist.barrier()
     torch.cuda.synchronize()
     r.reset_counters()
@@ -202,6 +232,7 @@ def main():
     for f in range(args.warmup, args.warmup + args.steps):
         step(f)
     if world > 1:
+        drain()  # every timed frame's gather is complete inside the timed region
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -209,10 +240,10 @@ def main():
     c = r.counters()
     rays = c["traverse_top"] + c["traverse_emitter"] + c["primary"]
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-        n = torch.tensor([rays], dtype=torch.float64, device="cuda")
+        n = torch.tensor([rays], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         rays = int(n.item())
 
@@ -228,7 +259,8 @@ def main():
         pix = W * rows
         alg = BYTES_PER_PIXEL.get(dom, 0) * pix
         achieved = alg / (timing[dom] * 1e-3) / 1e9
-        traffic = load_pmc_traffic(args.config, dom)
+        # the committed PMC numbers are per launch of a whole 1-GPU frame; a band launch differs
+        traffic = load_pmc_traffic(args.config, dom) if world == 1 else None
         result = {
             "metric": "Mrays/sec + ms/frame @1080p 1spp; cornell & city scenes, 1/2/4/8 GPU",
             "value": round(mrays, 2),
