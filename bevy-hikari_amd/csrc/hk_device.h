@@ -709,17 +709,46 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
 //   leaf:  (leaf box min, entry = payload | LEAF), (leaf box max, -)
 // Leaf boxes are the triangle's / instance's box, as the reference walk tests them.
 constexpr int GB_STACK = 64;
+// Stack entries (node, entry distance): the first GB_STACK_LDS live in the workgroup's LDS
+// (entry-major, one uint2 per thread per level: conflict-free), deeper ones in private scratch.
+constexpr int GB_STACK_LDS = 16;
 struct GbStack {
-    uint32_t node[GB_STACK];
-    float t[GB_STACK];
+    uint2* lds;  // [GB_STACK_LDS][blockDim.x], or null
+    uint32_t node[GB_STACK - GB_STACK_LDS];
+    float t[GB_STACK - GB_STACK_LDS];
     int sp;
+    HKD void push(uint32_t n, float tt)
+    {
+        if (lds && sp < GB_STACK_LDS) lds[sp * 256 + threadIdx.x] = make_uint2(n, __float_as_uint(tt));
+        else {
+            const int k = lds ? sp - GB_STACK_LDS : sp;
+            node[k] = n;
+            t[k] = tt;
+        }
+        sp++;
+    }
+    HKD void top(uint32_t& n, float& tt) const
+    {
+        if (lds && sp < GB_STACK_LDS) {
+            const uint2 e = lds[sp * 256 + threadIdx.x];
+            n = e.x;
+            tt = __uint_as_float(e.y);
+        } else {
+            const int k = lds ? sp - GB_STACK_LDS : sp;
+            n = node[k];
+            tt = t[k];
+        }
+    }
 };
 HKD bool gb_pop(GbStack& s, int base, float best, uint32_t& n)
 {
     while (s.sp > base) {
         s.sp--;
-        if (s.t[s.sp] < best) {
-            n = s.node[s.sp];
+        uint32_t m;
+        float tt;
+        s.top(m, tt);
+        if (tt < best) {
+            n = m;
             return true;
         }
     }
@@ -734,9 +763,7 @@ HKD bool gb_descend(GbStack& s, const Ray& ray, float4 a, float4 b, float4 c, fl
     const bool hl = tl < best, hr = tr < best;
     if (hl && hr) {
         const bool right_first = tr < tl;
-        s.node[s.sp] = right_first ? ls : rs;
-        s.t[s.sp] = right_first ? tl : tr;
-        s.sp++;
+        s.push(right_first ? ls : rs, right_first ? tl : tr);
         p = right_first ? rs : ls;
         return true;
     }
@@ -783,7 +810,7 @@ HKD void closest_bottom_ordered(const Scene& sc, GbStack& s, Hit& hit, const Ray
         if (!gb_pop(s, sbase, hit.distance, p)) return;
     }
 }
-HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray)
+HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = nullptr)
 {
     Hit hit;
     hit.uv = mk2(0.0f, 0.0f);
@@ -793,6 +820,7 @@ HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray)
     if (sc.n_instance_nodes == 0u) return hit;
     GbStack s;
     s.sp = 0;
+    s.lds = lds_stack;
     uint32_t p = 0u;
     for (;;) {
         const float4* w = sc.tlas_wide + 4u * (size_t)p;

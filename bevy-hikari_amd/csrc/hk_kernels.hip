@@ -59,6 +59,23 @@ HKD bool tile_pixel(uint32_t width, int32_t row0, int32_t rows, int32_t& x, int3
 #else
 #define HK_TRACE_OCC
 #endif
+// per-kernel overrides (waves per SIMD the register allocator must allow)
+#ifndef HK_DIRECT_WAVES
+#define HK_DIRECT_WAVES 0
+#endif
+#ifndef HK_INDIRECT_WAVES
+#define HK_INDIRECT_WAVES 0
+#endif
+#if HK_DIRECT_WAVES > 0
+#define HK_DIRECT_OCC __attribute__((amdgpu_waves_per_eu(HK_DIRECT_WAVES, 8)))
+#else
+#define HK_DIRECT_OCC HK_TRACE_OCC
+#endif
+#if HK_INDIRECT_WAVES > 0
+#define HK_INDIRECT_OCC __attribute__((amdgpu_waves_per_eu(HK_INDIRECT_WAVES, 8)))
+#else
+#define HK_INDIRECT_OCC HK_TRACE_OCC
+#endif
 
 // origin (global coordinates) of this workgroup's tile in the raster order
 HKD void tile_origin(int32_t row0, int32_t& x0, int32_t& y0)
@@ -87,6 +104,9 @@ extern __shared__ uint32_t hk_lds_scene[];
 template <bool LDS>
 __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewArgs V)
 {
+    // the traversal stack's first GB_STACK_LDS levels (32 KiB; the scene-staged variant keeps the
+    // whole stack in scratch so that scene + stack stay within the LDS budget)
+    __shared__ uint2 gb_lds_stack[LDS ? 1 : GB_STACK_LDS * 256];
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_GBUFFER>(A.sc, hk_lds_scene);
     else sc = A.sc;
@@ -100,7 +120,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
         ray.origin = ld3(V.world_position);
         ray.direction = primary_direction(V, (float)x + 0.5f, (float)y + 0.5f, A.F.S);
         ray.inv_direction = inv(ray.direction);
-        Hit hit = closest_hit_ordered(sc, ray);
+        Hit hit = closest_hit_ordered(sc, ray, LDS ? nullptr : gb_lds_stack);
         if (hit.instance_index == HK_U32_MAX) {
             A.G.position[idx] = make_float4(0, 0, 0, 0);
             A.G.normal[idx] = 0u;
@@ -282,7 +302,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
 }
 
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS>
-__global__ __launch_bounds__(256) HK_TRACE_OCC void k_direct(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, ChannelArgs C)
 {
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
@@ -456,7 +476,7 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
 }
 
 template <bool MULTI, bool LDS>
-__global__ __launch_bounds__(256) HK_TRACE_OCC void k_indirect(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, ChannelArgs C)
 {
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
