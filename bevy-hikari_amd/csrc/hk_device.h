@@ -1009,7 +1009,11 @@ HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 ra
         bool traced = false;
         if (dot(candidate.direction, normal) > 0.0f) {
             if (COUNT) n_emitter++;
+#ifdef HK_EXPERIMENT_NO_EMITTER_TRAVERSE  // timing experiment only (breaks parity)
+            traced = false;
+#else
             traced = traverse_bottom(sc, hit, r, ein.mesh.node[0], ein.mesh.node[1], ein.mesh.primitive, 0.0f);
+#endif
         }
         if (traced) {
             hit.instance_index = emissive.instance;
