@@ -258,6 +258,7 @@ def main():
         dom = max(per_frame, key=per_frame.get)
         pix = W * rows
         alg = BYTES_PER_PIXEL.get(dom, 0) * pix
+        frame_bytes = int(sum(BYTES_PER_PIXEL.get(k, 0) * {"denoise": 4}.get(k, 1) for k in timing) * pix * spp)
         achieved = alg / (timing[dom] * 1e-3) / 1e9
         # the committed PMC numbers are per launch of a whole 1-GPU frame; a band launch differs
         traffic = load_pmc_traffic(args.config, dom) if world == 1 else None
@@ -279,7 +280,12 @@ def main():
                        "parallelism": f"row-bands x{world} + RCCL all-gather" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg, "avg_ms": round(timing[dom], 4)},
+                         "algorithmic_bytes_per_launch": alg, "avg_ms": round(timing[dom], 4),
+                         # all kernels of a frame together (they overlap: the indirect chain runs on a
+                         # side stream next to direct/emissive, so per-kernel durations include sharing)
+                         "frame_algorithmic_bytes": frame_bytes,
+                         "frame_achieved": round(frame_bytes / (ms * 1e-3) / 1e9, 1),
+                         "frame_frac": round(frame_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
         }
         if world == 1 and args.cpu_budget > 0:
