@@ -560,10 +560,19 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         hk_sincos(px, &sn, &cs);
         f2 offset = mk2(py * cs, py * sn);
         int32_t scx = f2i32(offset.x + (float)x), scy = f2i32(offset.y + (float)y);
-        f2 suv = coords_to_uv_s(F, scx, scy);
-        if (suv.x < 0.0f || suv.y < 0.0f || suv.x > 1.0f || suv.y > 1.0f) continue;
         int32_t sdx, sdy;
-        jittered_coords(F, suv, sdx, sdy);
+        if (W.lds) {
+            // upscale ratio 1 and s == S (the window variant): the uv bounds test is the integer
+            // test (see k_denoise3), and jittered_coords(coords_to_uv(c)) == c: the jitter is
+            // (j * tx) * 0 and u32((c + 0.5) / S * S) truncates back to c for c < 2^22
+            if (scx < 0 || scy < 0 || scx >= (int32_t)F.s[0] || scy >= (int32_t)F.s[1]) continue;
+            sdx = scx;
+            sdy = scy;
+        } else {
+            f2 suv = coords_to_uv_s(F, scx, scy);
+            if (suv.x < 0.0f || suv.y < 0.0f || suv.x > 1.0f || suv.y > 1.0f) continue;
+            jittered_coords(F, suv, sdx, sdy);
+        }
         float sample_depth = win_depth(F, A.G, W, sdx, sdy);
         float depth_ratio = depth / sample_depth;
         if (depth_ratio < 0.9f || depth_ratio > 1.1f) continue;
@@ -743,8 +752,9 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         const int kk = k < 4 ? k : k + 1;  // skip the centre
         const int ox = kk % 3 - 1, oy = kk / 3 - 1;  // (-1,-1),(0,-1),(1,-1),(-1,0),(1,0),(-1,1),(0,1),(1,1)
         const int32_t sx = x + ox * step, sy = y + oy * step;
-        const f2 suv = coords_to_uv_s(F, sx, sy);
-        if (uv_outside(suv)) continue;
+        // uv_outside(coords_to_uv(s)) exactly: (sx + 0.5) / w < 0 iff sx < 0, and its rounding
+        // exceeds 1 iff sx >= w (for w < 2^24 the quotient is >= 1 + 2^-13 or <= 1 - 2^-25)
+        if (sx < 0 || sy < 0 || sx >= (int32_t)F.s[0] || sy >= (int32_t)F.s[1]) continue;
         const int32_t sidx = s_index(F, sx, sy);
         const float4 t0 = D.geom[2 * sidx];
         const float si = D.geom[2 * sidx + 1].x;
