@@ -28,6 +28,7 @@ sys.path.insert(0, str(ROOT / "bevy-hikari_amd"))
 
 # torch first: libhikari_amd.so then binds to the HIP runtime torch already loaded (same soname,
 # libamdhip64.so.7), so device pointers, streams and RCCL share one runtime in this process.
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -64,6 +65,12 @@ CONFIGS = {
     # configs[3]
     "city-4k": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True,
                     workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, row bands + RCCL all-gather"),
+    # city.rs with its emissive sphere rotating every frame (sphere_rotate_system, city.rs:290-294:
+    # rotate_local_z(0.2 rad/s x 1/60 s)): instances, TLAS, emissives and light BVH rebuilt on
+    # the GPU each frame (hk_update_instances) before rendering
+    "city-4k-dynamic": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, dynamic=True,
+                            workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, rotating "
+                                     "emissive sphere: GPU instance/TLAS/light-BVH rebuild every frame"),
     # per-frame fixed cost probe (launch / host overhead floor); not a BASELINE config
     "cornell-tiny-overhead": dict(scene="cornell", width=64, height=64, spatial=False, denoise=False,
                                   workload="examples/cornell.rs 64x64 (host/launch overhead probe)"),
@@ -185,7 +192,20 @@ def main():
     spp = cfg.get("spp", 1)
     shown = hikari_amd._abi.OUT_TONE_MAPPED if spp == 1 else hikari_amd._abi.OUT_ACCUMULATED
 
+    dynamic = cfg.get("dynamic", False)
+    if dynamic:
+        models0, aabbs = scene.instance_models(), scene.instance_local_aabbs()
+        sphere = [i for i, (m, _, _) in enumerate(scene.instances)
+                  if len(scene.meshes[m].positions) == 37 * 19][-1]  # the UV sphere (36 x 18 sectors)
+
     def step(f):
+        if dynamic:  # rotate_local_z(0.2 * dt): model = model0 * Rz(angle)
+            a = 0.2 * (f / 60.0)
+            rz = np.array([[np.cos(a), -np.sin(a), 0, 0], [np.sin(a), np.cos(a), 0, 0], [0, 0, 1, 0], [0, 0, 0, 1]])
+            models = models0.copy()
+            m0 = models0[sphere].reshape(4, 4).T  # column-major storage -> matrix
+            models[sphere] = (m0 @ rz).T.reshape(16).astype(np.float32)
+            r.update_instances(models, aabbs, sp)
         # one displayed frame = spp integrator sub-frames, each exactly one reference frame
         for k in range(spp):
             fi = frame_inputs(f * spp + k, cam, lights, W, H)
