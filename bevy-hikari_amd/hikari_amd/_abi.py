@@ -10,7 +10,7 @@ import os
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "libhikari_amd.so"
+LIB_PATH = Path(os.environ["HK_LIB"]) if os.environ.get("HK_LIB") else HERE / "libhikari_amd.so"  # HK_LIB: experiment builds
 
 HK_OK = 0
 HK_ERR_INVALID = -1

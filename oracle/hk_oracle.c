@@ -462,11 +462,25 @@ static Intersection intersects_triangle(const Ray* ray, const hk_primitive_verte
     return result;
 }
 
+#ifdef HKO_STATS
+/* traversal statistics (analysis builds only): [class][calls, tlas nodes, instances entered,
+ * blas nodes, triangle tests]; class 0 closest, 1 directional any-hit, 2 emissive any-hit,
+ * 3 emitter BLAS walk of select_light_candidate */
+unsigned long long hko_stats[4][5];
+static __thread int hko_class = 3;
+static __thread unsigned hko_ray_steps; /* node visits + leaf tests of the current traverse_top */
+uint32_t* hko_steps_out;                 /* per-ray steps of hko_trace, if set */
+#define HKO_STAT(k) (__atomic_fetch_add(&hko_stats[hko_class][k], 1ull, __ATOMIC_RELAXED), hko_ray_steps++)
+#else
+#define HKO_STAT(k) ((void)0)
+#endif
+
 static int traverse_bottom(const hko_ctx* c, Hit* hit, const Ray* ray, hk_mesh_index mesh, float early_distance)
 {
     int intersected = 0;
     uint32_t index = 0u;
     while (index < mesh.node[1]) {
+        HKO_STAT(3);
         uint32_t node_index = mesh.node[0] + index;
         const hk_node* node = &c->asset_nodes[node_index];
         Aabb aabb;
@@ -477,6 +491,7 @@ static int traverse_bottom(const hko_ctx* c, Hit* hit, const Ray* ray, hk_mesh_i
             aabb.min = min3(a, min3(b, d));
             aabb.max = max3(a, max3(b, d));
             if (intersects_aabb(ray, aabb) < hit->intersection.distance) {
+                HKO_STAT(4);
                 Intersection is = intersects_triangle(ray, vertices);
                 if (is.distance < hit->intersection.distance) {
                     hit->intersection = is;
@@ -499,6 +514,10 @@ static Hit traverse_top(const hko_ctx* c, Counts* cnt, const Ray* ray, float max
                         uint32_t exclude_instance)
 {
     cnt->top++;
+#ifdef HKO_STATS
+    hko_class = (max_distance == HK_F32_MAX && early_distance == 0.0f) ? 0 : (early_distance == 65535.0f ? 1 : 2);
+    HKO_STAT(0);
+#endif
     Hit hit;
     hit.intersection.uv = V2(0, 0);
     hit.intersection.distance = max_distance;
@@ -506,6 +525,7 @@ static Hit traverse_top(const hko_ctx* c, Counts* cnt, const Ray* ray, float max
     hit.primitive_index = HK_U32_MAX;
     uint32_t index = 0u;
     while (index < c->n_instance_nodes) {
+        HKO_STAT(1);
         const hk_node* node = &c->instance_nodes[index];
         Aabb aabb;
         if (node->entry_index >= HK_BVH_LEAF_FLAG) {
@@ -518,6 +538,7 @@ static Hit traverse_top(const hko_ctx* c, Counts* cnt, const Ray* ray, float max
                 r.origin = instance_position_world_to_local(instance, ray->origin);
                 r.direction = instance_direction_world_to_local(instance, ray->direction);
                 r.inv_direction = inv3(r.direction);
+                HKO_STAT(2);
                 if (traverse_bottom(c, &hit, &r, instance->mesh, early_distance)) {
                     hit.instance_index = instance_index;
                     if (hit.intersection.distance < early_distance) return hit;
@@ -715,6 +736,10 @@ static LightCandidate select_light_candidate(const Pass* P, Counts* cnt, v4 rand
         int traced = 0;
         if (dot3(candidate.direction, normal) > 0.0f) {
             cnt->emitter++;
+#ifdef HKO_STATS
+            hko_class = 3;
+            HKO_STAT(0);
+#endif
             traced = traverse_bottom(c, &hit, &r, emissive_instance->mesh, 0.0f);
         }
         if (traced) {
@@ -2147,6 +2172,9 @@ void hko_trace(hko_ctx* c, const float* rays, const float* max_distance, const f
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
     for (long long i = 0; i < (long long)n; ++i) {
         Counts k = {0, 0, 0};
+#ifdef HKO_STATS
+        hko_ray_steps = 0;
+#endif
         Ray ray;
         ray.origin = ld3(rays + 6 * i);
         ray.direction = ld3(rays + 6 * i + 3);
@@ -2160,6 +2188,9 @@ void hko_trace(hko_ctx* c, const float* rays, const float* max_distance, const f
         o[2] = hk_f2u(h.intersection.distance);
         o[3] = h.instance_index;
         o[4] = h.primitive_index;
+#ifdef HKO_STATS
+        if (hko_steps_out) hko_steps_out[i] = hko_ray_steps;
+#endif
     }
 }
 
