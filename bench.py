@@ -6,9 +6,11 @@ emissive and indirect temporal passes; spatial reuse and denoise off).  One "ste
 frame: primary-ray G-buffer + hk_render_frame + tone-sum (+ denoise when enabled).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the frame is
-split into N row bands (plus a recomputed halo when spatial reuse/denoise read neighbours);
-each rank renders its band and the tone-mapped RGBA16F bands are all-gathered over RCCL, so
-every rank ends each step with the whole frame.  Total work is fixed => "strong" scaling.
+split over the N ranks — interleaved 8-row stripes when no pass reads neighbours (config 2:
+balanced work), otherwise N contiguous row bands plus a recomputed halo (spatial reuse and the
+denoiser read up to 36 rows away); each rank renders its rows, the tone-mapped RGBA16F rows are
+all-gathered over RCCL (stripes are then put back in frame order on a side stream), so every
+rank ends each step with the whole frame.  Total work is fixed => "strong" scaling.
 
 Mrays/s = traversal queries issued for the frame's own pixels (primary rays + every
 traverse_top + every emitter traverse_bottom of select_light_candidate; device counters,
@@ -34,7 +36,7 @@ import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import band_of, halo_rows  # noqa: E402
+from hikari_amd.bands import band_of, halo_rows, stripe_gather_rows, use_stripes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -167,16 +169,21 @@ def main():
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
     s = st.to_c()
 
-    # row band of this rank (hikari_amd/bands.py)
-    b = band_of(rank, world, H)
-    band = b.rows
+    # rows of this rank (hikari_amd/bands.py): interleaved stripes, or a contiguous band + halo
+    stripes = world > 1 and use_stripes(cfg["spatial"], cfg["denoise"])
     r = HikariRenderer(device)
     r.set_noise()
     r.upload_scene(scene)
     r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
-    if world > 1:
+    if stripes:
+        r.resize_striped(W, H, rank, world)
+        band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
+    elif world > 1:
+        b = band_of(rank, world, H)
+        band = b.rows
         r.resize(W, H, 1.0, b.y0, b.rows)
     else:
+        band = H
         r.resize(W, H, 1.0)
     row0, rows, core0, core_rows = r.band_info()
 
@@ -184,10 +191,15 @@ def main():
     sp = stream.cuda_stream
     # double-buffered band / gathered frame: the all-gather of frame f runs on RCCL's stream
     # while frame f+1 renders; a buffer is reused only after its previous gather completed
-    band_t = [torch.empty((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
+    band_t = [torch.zeros((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
     full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
         if world > 1 else None
     pending = [None, None]
+    if stripes:  # stripes back in frame order, on a side stream after each gather
+        frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
+        index_t = torch.from_numpy(gather_index).to("cuda")
+        side = torch.cuda.Stream()
+        reorder_done = [None, None]
 
     spp = cfg.get("spp", 1)
     shown = hikari_amd._abi.OUT_TONE_MAPPED if spp == 1 else hikari_amd._abi.OUT_ACCUMULATED
@@ -222,6 +234,8 @@ def main():
             k = f & 1
             if pending[k] is not None:
                 pending[k].wait()  # device-side: the stream waits for that gather
+            if stripes and reorder_done[k] is not None:
+                stream.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
             r.copy_output_rows(shown, core0, core_rows, band_t[k].data_ptr(), False, sp)
             if rehearsal:
                 parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
@@ -229,12 +243,22 @@ def main():
                 full_t[k].copy_(torch.cat(parts))
             else:
                 pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
+            if stripes:
+                with torch.cuda.stream(side):
+                    if pending[k] is not None:
+                        pending[k].wait()
+                    else:
+                        side.wait_stream(stream)
+                    torch.index_select(full_t[k], 0, index_t, out=frame_t[k])
+                    reorder_done[k] = side.record_event()
 
     def drain():
         for k in range(2):
             if pending[k] is not None:
                 pending[k].wait()
                 pending[k] = None
+        if stripes:
+            torch.cuda.current_stream().wait_stream(side)
 
     for f in range(args.warmup):
         step(f)
@@ -297,7 +321,8 @@ def main():
             "data": "synthetic (static camera; reference assets: cornell.glb, blue noise)",
             "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": spp,
                        "rays_per_frame": int(rays // args.steps),
-                       "parallelism": f"row-bands x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+                       "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
+                                       f"row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg, "avg_ms": round(timing[dom], 4),

@@ -157,6 +157,10 @@ struct Frame {
     int32_t s_row0, s_rows;  // integrator-plane band
     int32_t count_y0, count_y1;    // global integrator rows whose rays are counted (the band's own rows)
     int32_t count_Sy0, count_Sy1;  // the same for the full-resolution G-buffer rows
+    // interleaved stripes (stripe_n >= 2): the local planes hold the STRIPE_H-row stripes
+    // k, k + n, k + 2n, ... of the frame (stripe_k = k) instead of one contiguous band; only for
+    // passes without neighbour reads (no halo), see hk_resize_striped
+    int32_t stripe_n, stripe_k;
     // host-evaluated constants (same IEEE expressions, so bit-identical to computing them here)
     float inv_S[2];                // 1 / S (jittered_uv texel size)
     float inv_s[2];                // RN(1 / s): div_by() reciprocals of the integrator size
@@ -296,49 +300,69 @@ HKD bool in_frame(int32_t x, int32_t y, const uint32_t* size)
 {
     return x >= 0 && y >= 0 && (uint32_t)x < size[0] && (uint32_t)y < size[1];
 }
-HKD int32_t band_index(int32_t x, int32_t y, uint32_t width, int32_t row0, int32_t rows)
+constexpr int32_t STRIPE_H = 8;  // rows per interleaved stripe (one wave tile high)
+// local plane row of global row y: band offset, or the stripe map; rows this context does not
+// hold clamp into the local plane (they only feed discarded halo pixels / motion edges)
+HKD int32_t local_row(const Frame& F, int32_t y, int32_t row0)
 {
-    int32_t ly = y - row0;
+    if (F.stripe_n >= 2) {
+        const int32_t t = y / STRIPE_H;
+        return (t / F.stripe_n) * STRIPE_H + (y - t * STRIPE_H);
+    }
+    return y - row0;
+}
+// global row of local plane row ly
+HKD int32_t global_row(const Frame& F, int32_t ly, int32_t row0)
+{
+    if (F.stripe_n >= 2) {
+        const int32_t t = ly / STRIPE_H;
+        return (t * F.stripe_n + F.stripe_k) * STRIPE_H + (ly - t * STRIPE_H);
+    }
+    return row0 + ly;
+}
+HKD int32_t band_index(const Frame& F, int32_t x, int32_t y, uint32_t width, int32_t row0, int32_t rows)
+{
+    int32_t ly = local_row(F, y, row0);
     ly = ly < 0 ? 0 : (ly >= rows ? rows - 1 : ly);
     return x + (int32_t)width * ly;
 }
 HKD f4 load_position(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return mk4(0, 0, 0, 0);
-    float4 p = G.position[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    float4 p = G.position[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)];
     return mk4(p.x, p.y, p.z, p.w);
 }
 HKD float load_depth(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return 0.0f;
-    return G.position[band_index(x, y, F.S[0], F.S_row0, F.S_rows)].w;
+    return G.position[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)].w;
 }
 HKD f3 load_normal(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return mk3(0, 0, 0);
-    uint32_t n = G.normal[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    uint32_t n = G.normal[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)];
     return mk3(hk_unpack_snorm8(n, 0), hk_unpack_snorm8(n, 1), hk_unpack_snorm8(n, 2));
 }
 HKD f2 load_instance_material(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return mk2(0, 0);
-    float2 v = G.instance_material[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    float2 v = G.instance_material[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)];
     return mk2(v.x, v.y);
 }
 HKD f4 load_velocity_uv(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return mk4(0, 0, 0, 0);
-    float4 v = G.velocity_uv[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    float4 v = G.velocity_uv[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)];
     return mk4(v.x, v.y, v.z, v.w);
 }
 HKD f2 load_depth_gradient(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return mk2(0, 0);
-    float2 v = G.depth_gradient[band_index(x, y, F.S[0], F.S_row0, F.S_rows)];
+    float2 v = G.depth_gradient[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)];
     return mk2(v.x, v.y);
 }
 // integrator-plane (s) index of an in-frame pixel
-HKD int32_t s_index(const Frame& F, int32_t x, int32_t y) { return band_index(x, y, F.s[0], F.s_row0, F.s_rows); }
+HKD int32_t s_index(const Frame& F, int32_t x, int32_t y) { return band_index(F, x, y, F.s[0], F.s_row0, F.s_rows); }
 
 HKD f2 coords_to_uv(int32_t x, int32_t y, const uint32_t* size)
 {

@@ -31,7 +31,7 @@ namespace hk {
 // XCD-stripe order (cdna_hip_programming.md T1, bijective form): workgroup L runs on XCD L % 8,
 // and each XCD gets a contiguous range of tiles in raster order, so the taps hit its own L2.
 template <bool XCD_STRIPES = false>
-HKD bool tile_pixel(uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
+HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
 {
     const uint32_t gx = gridDim.x;
     const uint32_t L = blockIdx.x + blockIdx.y * gx;
@@ -46,7 +46,7 @@ HKD bool tile_pixel(uint32_t width, int32_t row0, int32_t rows, int32_t& x, int3
     uint32_t w = t >> 6, lane = t & 63u;
     x = (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
     int32_t ly = (int32_t)(ty * 16u + (w >> 1) * 8u + (lane >> 3));
-    y = row0 + ly;
+    y = global_row(F, ly, row0);
     return (uint32_t)x < width && ly < rows;
 }
 
@@ -111,11 +111,11 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
     if constexpr (LDS) sc = stage_scene<PLAN_GBUFFER>(A.sc, hk_lds_scene);
     else sc = A.sc;
     int32_t x, y;
-    bool active = tile_pixel(A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
+    bool active = tile_pixel(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
     uint32_t n_primary = 0;
     if (active) {
         n_primary = 1;
-        int32_t idx = x + (int32_t)A.F.S[0] * (y - A.F.S_row0);
+        int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
         Ray ray;
         ray.origin = ld3(V.world_position);
         ray.direction = primary_direction(V, (float)x + 0.5f, (float)y + 0.5f, A.F.S);
@@ -164,8 +164,8 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
 __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
 {
     int32_t x, y;
-    if (!tile_pixel(A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
-    int32_t idx = x + (int32_t)A.F.S[0] * (y - A.F.S_row0);
+    if (!tile_pixel(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
+    int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
     f4 pd = load_position(A.F, A.G, x, y);
     if (pd.w < HK_F32_EPSILON) {
         store_rgba16f(albedo, idx, mk4(0, 0, 0, 0));
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+    if (tile_pixel(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_body<EMISSIVE_LIT, RENDER_EMISSIVE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+    if (tile_pixel(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_spatial(FrameArgs A, Chann
         W.lds = win;
     }
     int32_t x, y;
-    if (tile_pixel(A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y, W);
+    if (tile_pixel(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y, W);
 }
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
@@ -657,7 +657,7 @@ HKD bool bad3(f3 v)
 // albedo plane is S-sized (band-local rows)
 HKD f4 load_albedo(const Frame& F, const uint2* albedo, int32_t x, int32_t y)
 {
-    return load_rgba16f(albedo, band_index(x, y, F.S[0], F.S_row0, F.S_rows));
+    return load_rgba16f(albedo, band_index(F, x, y, F.S[0], F.S_row0, F.S_rows));
 }
 
 // Channel-fused denoiser.  The reference runs demodulation + 4 levels separately for each
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<true>(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<true>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     f2 uv = coords_to_uv(x, y, F.s);
     f2 duv = jittered_uv(F, uv, 0.5f);
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<true>(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<true>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     constexpr int32_t step = 8 >> LEVEL;
     const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<true>(F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<true>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     f4 c = load_rgba16f(T.direct, idx);
     f4 e = load_rgba16f(T.emissive, idx);

@@ -62,6 +62,7 @@ struct hk_ctx {
     int32_t S_row0 = 0, S_rows = 0, s_row0 = 0, s_rows = 0;
     int32_t core_row0 = 0, core_rows = 0;
     int32_t halo = BAND_HALO;
+    int32_t stripe_n = 0, stripe_k = 0;  // interleaved stripes (hk_resize_striped), stripe_n >= 2
     bool sized = false;
 
     // G-buffer (band-local, S-wide)
@@ -302,6 +303,13 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     F.count_Sy0 = c->S_row0 + c->core_row0;
     F.count_Sy1 = c->S_rows == (int32_t)c->S[1] && c->core_rows == (int32_t)c->s[1] ? (int32_t)c->S[1]
                                                                                       : F.count_Sy0 + c->core_rows;
+    F.stripe_n = c->stripe_n;
+    F.stripe_k = c->stripe_k;
+    if (c->stripe_n >= 2) {  // every local row is one of this context's own rows
+        F.count_y0 = F.count_Sy0 = 0;
+        F.count_y1 = (int32_t)c->s[1];
+        F.count_Sy1 = (int32_t)c->S[1];
+    }
     A.G.position = c->g_position;
     A.G.normal = c->g_normal;
     A.G.depth_gradient = c->g_depth_gradient;
@@ -632,7 +640,23 @@ int hk_set_noise(hk_ctx* c, const uint8_t* rgba, uint32_t count, uint32_t size)
     return HK_OK;
 }
 
+static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows,
+                       uint32_t stripe_n, uint32_t stripe_k);
+
 int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows)
+{
+    return resize_impl(c, width, height, ratio, band_y0, band_rows, 0u, 0u);
+}
+
+int hk_resize_striped(hk_ctx* c, uint32_t width, uint32_t height, uint32_t rank, uint32_t world)
+{
+    if (!c || world == 0 || rank >= world) return HK_ERR_INVALID;
+    if (world == 1) return resize_impl(c, width, height, 1.0f, 0u, 0u, 0u, 0u);
+    return resize_impl(c, width, height, 1.0f, 0u, 0u, world, rank);
+}
+
+static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows,
+                       uint32_t stripe_n, uint32_t stripe_k)
 {
     if (!c || width == 0 || height == 0) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
@@ -644,6 +668,14 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
     if (band_y0 + band_rows > height) return fail(c, HK_ERR_INVALID, "band outside the frame");
     bool whole = band_y0 == 0 && band_rows == height;
     if (!whole && ratio != 1.0f) return fail(c, HK_ERR_INVALID, "row bands require upscale ratio 1.0");
+    uint32_t stripe_rows = 0;  // rows of stripes k, k + n, ... (STRIPE_H rows each, the last one may be short)
+    if (stripe_n >= 2) {
+        if (stripe_n > (height + STRIPE_H - 1) / STRIPE_H)
+            return fail(c, HK_ERR_INVALID, "more stripe ranks than stripes in the frame");
+        for (uint32_t t = stripe_k; t * STRIPE_H < height; t += stripe_n)
+            stripe_rows += height - t * STRIPE_H < (uint32_t)STRIPE_H ? height - t * STRIPE_H : (uint32_t)STRIPE_H;
+        whole = false;
+    }
     HK_HIP(c, hipStreamSynchronize(c->stream));
     free_targets(c);
     c->S[0] = width;
@@ -652,7 +684,14 @@ int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t 
     float scale = 1.0f / ratio;  // light.rs:318-319: ceil(scale * size)
     c->s[0] = (uint32_t)std::ceil(scale * (float)width);
     c->s[1] = (uint32_t)std::ceil(scale * (float)height);
-    if (whole) {
+    c->stripe_n = (int32_t)stripe_n;
+    c->stripe_k = (int32_t)stripe_k;
+    if (stripe_n >= 2) {
+        c->S_row0 = c->s_row0 = 0;
+        c->S_rows = c->s_rows = (int32_t)stripe_rows;
+        c->core_row0 = 0;
+        c->core_rows = (int32_t)stripe_rows;
+    } else if (whole) {
         c->S_row0 = 0;
         c->S_rows = (int32_t)height;
         c->s_row0 = 0;
@@ -813,6 +852,8 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
+        return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     c->head = in->frame_number & 1u;
     FrameArgs A = frame_args(c, settings, in);
     // The indirect channel owns reservoir buffers 6-9 (light.rs:518-546 pairs (6,8)); direct and
@@ -853,6 +894,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     if (rc) return rc;
     if (!settings || !in) return fail(c, HK_ERR_INVALID, "null settings or frame inputs");
     if (!settings->denoise) return HK_OK;
+    if (c->stripe_n >= 2) return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude the denoiser: it reads neighbours");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
     FrameArgs A = frame_args(c, settings, in);

@@ -137,6 +137,7 @@ def lib() -> C.CDLL:
         "hk_texture_upload": (i32, [vp, vp, u32]),
         "hk_resize": (i32, [vp, u32, u32, C.c_float, u32, u32]),
         "hk_set_band_halo": (i32, [vp, u32]),
+        "hk_resize_striped": (i32, [vp, u32, u32, u32, u32]),
         "hk_band_info": (i32, [vp] + [C.POINTER(C.c_int32)] * 4),
         "hk_copy_output_rows": (i32, [vp, i32, u32, u32, vp, i32, vp]),
         "hk_render_gbuffer": (i32, [vp, C.POINTER(hk_frame_inputs), vp]),
@@ -181,7 +182,7 @@ def lib() -> C.CDLL:
 # symbols include/*.h declare (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
-    "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
+    "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
     "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
+
 SPATIAL_REACH = 20  # light.wgsl:251 SPATIAL_REUSE_RANGE (indirect); emissive uses 10
 ATROUS_REACH = 8 + 4 + 2 + 1  # denoise.wgsl:101-114 step sizes of levels 0..3
 VARIANCE_REACH = 1  # denoise.wgsl:151-159 3x3 variance blur
@@ -36,3 +38,34 @@ def band_of(rank: int, world: int, height: int) -> Band:
         raise ValueError(f"frame height {height} does not split into {world} equal bands")
     rows = height // world
     return Band(rank, world, rank * rows, rows)
+
+
+# ---------------------------------------------------------------- interleaved stripes
+# Frames without neighbour reads (spatial reuse and denoise off, halo 0) are split into 8-row
+# stripes dealt round-robin to the ranks (hk_resize_striped): every rank gets an equal share of
+# every screen region, so the ranks' work is balanced where contiguous bands are not (cornell:
+# the box fills the middle rows, the top and bottom bands are mostly background).
+STRIPE_H = 8  # hk_device.h STRIPE_H
+
+
+def stripe_rows(rank: int, world: int, height: int) -> np.ndarray:
+    """Global rows held by `rank`, in local-row order."""
+    rows = [np.arange(t * STRIPE_H, min(height, (t + 1) * STRIPE_H))
+            for t in range(rank, (height + STRIPE_H - 1) // STRIPE_H, world)]
+    return np.concatenate(rows) if rows else np.zeros(0, np.int64)
+
+
+def stripe_gather_rows(world: int, height: int) -> tuple:
+    """(padded rows per rank, index) for reassembling an all-gather of stripe planes: every rank
+    contributes `pad` rows (its stripes, zero-padded), and frame row y = gathered row index[y]."""
+    per = [stripe_rows(k, world, height) for k in range(world)]
+    pad = max(len(p) for p in per)
+    index = np.empty(height, np.int64)
+    for k, p in enumerate(per):
+        index[p] = k * pad + np.arange(len(p))
+    return pad, index
+
+
+def use_stripes(spatial_reuse: bool, denoise: bool) -> bool:
+    """Stripes where no pass reads neighbours; contiguous bands + halo otherwise."""
+    return halo_rows(spatial_reuse, denoise) == 0

@@ -66,6 +66,11 @@ class HikariRenderer:
         _check(self.ctx, self._L.hk_resize(self.ctx, width, height, ratio, band_y0, band_rows), "hk_resize")
         self.width, self.height = width, height
 
+    def resize_striped(self, width: int, height: int, rank: int, world: int) -> None:
+        """Interleaved 8-row stripes rank, rank + world, ... of the frame (bands.stripes_of)."""
+        _check(self.ctx, self._L.hk_resize_striped(self.ctx, width, height, rank, world), "hk_resize_striped")
+        self.width, self.height = width, height
+
     def set_band_halo(self, rows: int) -> None:
         _check(self.ctx, self._L.hk_set_band_halo(self.ctx, rows), "hk_set_band_halo")
 

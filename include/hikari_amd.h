@@ -219,6 +219,15 @@ int hk_texture_upload(hk_ctx* ctx, const hk_texture* textures, uint32_t count);
 int hk_resize(hk_ctx* ctx, uint32_t width, uint32_t height, float upscale_ratio,
               uint32_t band_y0, uint32_t band_rows);
 
+/* Interleaved-stripe decomposition for N GPUs (no reference counterpart: the reference renders
+ * on one device).  The context holds the 8-row stripes rank, rank + world, rank + 2 world, ... of a
+ * width x height frame (upscale ratio 1.0), so every rank gets an equal share of every screen
+ * region: balanced work where contiguous bands are not (cornell: the box fills the middle rows).
+ * Only for frames without neighbour reads — spatial reuse and the denoiser return HK_ERR_STATE in
+ * this mode; those use contiguous bands + halo (hk_resize with band rows).  Local row l holds
+ * global row (l / 8 * world + rank) * 8 + l % 8; hk_band_info reports row0 = 0, rows = core_rows
+ * = the local row count.  world == 1 is hk_resize of the whole frame. */
+int hk_resize_striped(hk_ctx* ctx, uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
 /* rows of halo recomputed above and below a band by hk_resize (default 40, enough for spatial
  * reuse + 4 a-trous levels + the variance blur: 20 + 15 + 1); 0 is exact when spatial reuse and
  * denoise are both off.  Call before hk_resize. */

@@ -140,6 +140,56 @@ def test_gpu_row_bands_match_whole_frame(spatial, denoise):
     assert total == o.counters()
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_interleaved_stripes_match_whole_frame(world):
+    """Interleaved 8-row stripe contexts (bench.py's decomposition for frames without neighbour
+    reads, run on one GPU) reassemble the whole-frame oracle render bit-exactly, count exactly
+    the whole frame's rays, and refuse the passes that read neighbours."""
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
+    from hikari_amd._abi import HikariError
+    from hikari_amd.bands import stripe_gather_rows
+    from oracle import Oracle
+    W, H = 64, 100  # 13 stripes, the last one 4 rows
+    scene, cam, lights = examples.cornell()
+    desc = scene.build()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=False, denoise=False)
+    s = st.to_c()
+    o = Oracle(desc, load_noise(), W, H, 1.0)
+    ranks = []
+    for k in range(world):
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.resize_striped(W, H, k, world)
+        ranks.append(r)
+    for f in range(5):
+        fi = frame_inputs(f, cam, lights, W, H)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.tone_sum(s)
+        for r in ranks:
+            r.render_gbuffer(fi)
+            r.render_frame(s, fi)
+            r.denoise(s, fi)  # denoise off: a no-op, allowed
+            r.tone_sum(s)
+    pad, index = stripe_gather_rows(world, H)
+    gathered = np.zeros((world * pad, W, 8), np.uint8)
+    total = {"traverse_top": 0, "traverse_emitter": 0, "primary": 0}
+    for k, r in enumerate(ranks):
+        row0, rows, core0, core_rows = r.band_info()
+        assert row0 == 0 and core0 == 0 and rows == core_rows
+        gathered[k * pad: k * pad + rows] = r.output(10)
+        for name, v in r.counters().items():
+            total[name] += v
+    assert np.array_equal(canon_plane(10, gathered[index]), canon_plane(10, o.output(10)))
+    assert total == o.counters()
+    spatial = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=True).to_c()
+    with pytest.raises(HikariError):
+        ranks[0].render_frame(spatial, frame_inputs(5, cam, lights, W, H))
+    with pytest.raises(HikariError):
+        ranks[0].denoise(spatial, frame_inputs(5, cam, lights, W, H))
+
+
 def _gpu_factory(w, h, ratio=1.0):
     def make(scene, desc):
         from hikari_amd import HikariRenderer

@@ -1,0 +1,77 @@
+"""Per-rank compute time of the row-band decomposition, measured on ONE GPU (development aid).
+
+For N in 1, 2, 4, 8 a renderer holds the band a rank of an N-GPU run renders (band rows + halo)
+and runs the bench workload on it; the slowest band's ms/frame is the per-GPU compute floor of
+the N-GPU frame (the RCCL all-gather of frame f overlaps frame f+1 in bench.py).  This projects
+the strong-scaling curve when no multi-GPU box is at hand; it is not a multi-GPU measurement.
+Frames without neighbour reads use bench.py's interleaved stripes (--bands: contiguous bands).
+usage: python tools/band_scaling.py [config] [steps] [--bands]"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "bevy-hikari_amd"))
+import bench  # noqa: E402
+from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
+from hikari_amd.bands import band_of, halo_rows, use_stripes  # noqa: E402
+
+cfg_name = sys.argv[1] if len(sys.argv) > 1 else "cornell-1080p-nee"
+steps = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 50
+cfg = bench.CONFIGS[cfg_name]
+W, H = cfg["width"], cfg["height"]
+scene, cam, lights = examples.SCENES[cfg["scene"]]()
+scene.build()
+st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
+s = st.to_c()
+torch.cuda.set_device(0)
+sp = torch.cuda.current_stream().cuda_stream
+out = {"config": cfg_name, "resolution": [W, H], "bands": {}}
+for n in (1, 2, 4, 8):
+    worst = 0.0
+    stripes = use_stripes(cfg["spatial"], cfg["denoise"]) and "--bands" not in sys.argv
+    for rank in sorted({0, n // 2, n - 1}):  # edge and middle bands
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
+        if n == 1:
+            r.resize(W, H, 1.0)
+        elif stripes:
+            r.resize_striped(W, H, rank, n)
+        else:
+            b = band_of(rank, n, H)
+            r.resize(W, H, 1.0, b.y0, b.rows)
+
+        def step(f):
+            fi = frame_inputs(f, cam, lights, W, H)
+            r.render_gbuffer(fi, sp)
+            r.render_frame(s, fi, sp)
+            if st.denoise:
+                r.denoise(s, fi, sp)
+            r.tone_sum(s, sp)
+
+        for f in range(10):
+            step(f)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for f in range(10, 10 + steps):
+            step(f)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        worst = max(worst, ms)
+        if "--kernels" in sys.argv and rank == n // 2:
+            r.enable_kernel_timing(True)
+            for f in range(10 + steps, 20 + steps):
+                step(f)
+            torch.cuda.synchronize()
+            print(f"  N={n} rank {rank} kernel ms:", {k: round(v, 4) for k, v in r.kernel_timing().items()}, flush=True)
+            r.enable_kernel_timing(False)
+        r.close()
+    out["bands"][n] = round(worst, 4)
+    print(f"N={n}: slowest band {worst:.4f} ms/frame  (projected speedup {out['bands'][1] / worst:.2f}x)", flush=True)
+print(json.dumps(out))
