@@ -42,7 +42,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 # Compulsory HBM bytes per pixel per launch (reference texel formats; DESIGN.md "Roofline"):
 BYTES_PER_PIXEL = {
-    "gbuffer": 52,                   # writes position 16 + normal 4 + gradient 8 + ids 8 + velocity/uv 16
+    "gbuffer": 60,                   # writes position 16 + normal 4 + gradient 8 + ids 8 + velocity/uv 16
+                                     # + the fused full_screen_albedo's RGBA16F 8
     "full_screen_albedo": 52,        # reads 44 B of G-buffer, writes RGBA16F
     "direct_lit": 184,               # G 44 + reservoir read 64 + write 64 + variance 4 + render 8
     "direct_emissive": 184,

@@ -101,8 +101,23 @@ HKD float ndc_depth(const float* vp, f3 p)
 
 extern __shared__ uint32_t hk_lds_scene[];
 
+// full_screen_albedo (light.wgsl:1019-1042) of one deferred pixel from the G-buffer values as
+// they are stored (snorm8 normal, f32 position, material id and uv): k_albedo, and fused into
+// k_gbuffer, which has them in registers.
+HKD f4 albedo_of(const Frame& F, const Scene& sc, f4 pd, uint32_t packed_normal, float material_f, f2 uv)
+{
+    if (pd.w < HK_F32_EPSILON) return mk4(0, 0, 0, 0);
+    const f3 normal = mk3(hk_unpack_snorm8(packed_normal, 0), hk_unpack_snorm8(packed_normal, 1),
+                          hk_unpack_snorm8(packed_normal, 2));
+    const Surface surface = retreive_surface(sc, f2u32(material_f), uv);
+    const f3 view_direction = calculate_view(F, mk4(pd.x, pd.y, pd.z, 1.0f));
+    const f3 a = env_brdf(view_direction, normal, surface);
+    return mk4(a.x, a.y, a.z, 1.0f);
+}
+
+// albedo != null: the frame's full_screen_albedo is written here too (hk_render_frame skips it)
 template <bool LDS>
-__global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewArgs V)
+__global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewArgs V, uint2* albedo)
 {
     // the traversal stack's first GB_STACK_LDS levels (32 KiB; the scene-staged variant keeps the
     // whole stack in scratch so that scene + stack stay within the LDS budget)
@@ -127,12 +142,18 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
             A.G.depth_gradient[idx] = make_float2(0, 0);
             A.G.instance_material[idx] = make_float2(0, 0);
             A.G.velocity_uv[idx] = make_float4(0, 0, 0, 0);
+            if (albedo) store_rgba16f(albedo, idx, mk4(0, 0, 0, 0));
         } else {
             HitInfo info = hit_info(sc, ray, hit);
             f3 p = xyz(info.position);
             float depth = ndc_depth(V.view_proj, p);
             A.G.position[idx] = make_float4(p.x, p.y, p.z, depth);
-            A.G.normal[idx] = hk_pack4x8snorm(info.normal.x, info.normal.y, info.normal.z, 1.0f);
+            const uint32_t packed_normal = hk_pack4x8snorm(info.normal.x, info.normal.y, info.normal.z, 1.0f);
+            A.G.normal[idx] = packed_normal;
+            if (albedo)
+                store_rgba16f(albedo, idx,
+                              albedo_of(A.F, A.sc, mk4(p.x, p.y, p.z, depth), packed_normal,
+                                        (float)info.material_index + 0.5f, info.uv));
             const hk_instance& in = get_instance(sc, hit.instance_index);
             f3 t0, t1, t2;
             load_triangle(sc.primitives, hit.primitive_index, t0, t1, t2);
@@ -165,19 +186,15 @@ __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
 {
     int32_t x, y;
     if (!tile_pixel(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
-    int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
-    f4 pd = load_position(A.F, A.G, x, y);
+    const int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
+    const f4 pd = load_position(A.F, A.G, x, y);
     if (pd.w < HK_F32_EPSILON) {
         store_rgba16f(albedo, idx, mk4(0, 0, 0, 0));
         return;
     }
-    f3 normal = load_normal(A.F, A.G, x, y);
-    uint32_t material = f2u32(load_instance_material(A.F, A.G, x, y).y);
     const f4 velocity_uv = load_velocity_uv(A.F, A.G, x, y);
-    Surface surface = retreive_surface(A.sc, material, mk2(velocity_uv.z, velocity_uv.w));
-    f3 view_direction = calculate_view(A.F, mk4(pd.x, pd.y, pd.z, 1.0f));
-    f3 a = env_brdf(view_direction, normal, surface);
-    store_rgba16f(albedo, idx, mk4(a.x, a.y, a.z, 1.0f));
+    store_rgba16f(albedo, idx, albedo_of(A.F, A.sc, pd, A.G.normal[idx], load_instance_material(A.F, A.G, x, y).y,
+                                         mk2(velocity_uv.z, velocity_uv.w)));
 }
 
 // ------------------------------------------------------------------ direct_lit (light.wgsl:1044-1261)
@@ -868,11 +885,11 @@ static uint32_t lds_plan_bytes(const FrameArgs& A, int plan, bool preferred)
     return b <= LDS_SCENE_MAX ? b : 0u;
 }
 
-void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, hipStream_t st)
+void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, hipStream_t st)
 {
     const uint32_t lds = lds_plan_bytes(A, PLAN_GBUFFER, false);
-    if (lds) hipLaunchKernelGGL(k_gbuffer<true>, tiles(A.F.S[0], A.F.S_rows), dim3(256), lds, st, A, V);
-    else hipLaunchKernelGGL(k_gbuffer<false>, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, V);
+    if (lds) hipLaunchKernelGGL(k_gbuffer<true>, tiles(A.F.S[0], A.F.S_rows), dim3(256), lds, st, A, V, albedo);
+    else hipLaunchKernelGGL(k_gbuffer<false>, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, V, albedo);
 }
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st)
 {

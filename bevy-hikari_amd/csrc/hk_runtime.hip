@@ -63,6 +63,7 @@ struct hk_ctx {
     int32_t core_row0 = 0, core_rows = 0;
     int32_t halo = BAND_HALO;
     int32_t stripe_n = 0, stripe_k = 0;  // interleaved stripes (hk_resize_striped), stripe_n >= 2
+    bool albedo_fresh = false;  // the albedo target matches the G-buffer (k_gbuffer wrote both)
     bool sized = false;
 
     // G-buffer (band-local, S-wide)
@@ -678,6 +679,7 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     }
     HK_HIP(c, hipStreamSynchronize(c->stream));
     free_targets(c);
+    c->albedo_fresh = false;
     c->S[0] = width;
     c->S[1] = height;
     c->ratio = ratio;
@@ -792,7 +794,10 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     for (int i = 0; i < 3; ++i) V.world_position[i] = in->view.world_position[i];
     std::memcpy(V.view_proj, in->view.view_proj, sizeof(V.view_proj));
     std::memcpy(V.inverse_view_proj, in->view.inverse_view_proj, sizeof(V.inverse_view_proj));
-    timed(c, "gbuffer", st, [&] { launch_gbuffer(A, V, st); });
+    // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
+    // hk_render_frame runs it on its own only for host-supplied G-buffers
+    timed(c, "gbuffer", st, [&] { launch_gbuffer(A, V, c->albedo, st); });
+    c->albedo_fresh = true;
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -801,6 +806,7 @@ int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, i
 {
     if (!c || !data) return HK_ERR_INVALID;
     if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    c->albedo_fresh = false;
     size_t SP = (size_t)c->S[0] * c->S_rows;
     void* dst = nullptr;
     size_t need = 0;
@@ -870,7 +876,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         HK_HIP(c, hipEventRecord(c->ev_fork, st));
         HK_HIP(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
     }
-    timed(c, "full_screen_albedo", st, [&] { launch_albedo(A, c->albedo, st); });
+    if (!c->albedo_fresh) timed(c, "full_screen_albedo", st, [&] { launch_albedo(A, c->albedo, st); });
     ChannelArgs C0 = channel(c, A.F.number, 0);
     timed(c, "direct_lit", st, [&] { launch_direct(A, C0, false, st); });
     ChannelArgs C1 = channel(c, A.F.number, 1);
