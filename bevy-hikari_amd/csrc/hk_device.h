@@ -855,39 +855,9 @@ HKD bool gb_descend(GbStack& s, const Ray& ray, float4 a, float4 b, float4 c, fl
     }
     return false;
 }
-HKD void closest_bottom_ordered(const Scene& sc, GbStack& s, Hit& hit, const Ray& ray, const hk_instance& in,
-                                uint32_t instance_index)
-{
-    const int sbase = s.sp;
-    const uint32_t base = in.mesh.node[0];
-    if (in.mesh.node[1] == 0u) return;
-    uint32_t p = 0u;  // mesh-local subtree start
-    for (;;) {
-        const float4* w = sc.blas_wide + 4u * (size_t)(base + p);
-        const float4 a = w[0], b = w[1];
-        const uint32_t entry = __float_as_uint(a.w);
-        bool go = false;
-        if (entry >= HK_BVH_LEAF_FLAG) {
-            if (intersects_aabb(ray, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance) {
-                const uint32_t primitive_index = in.mesh.primitive + entry - HK_BVH_LEAF_FLAG;
-                f3 t0, t1, t2;
-                load_triangle(sc.primitives, primitive_index, t0, t1, t2);
-                f2 uv;
-                const float dd = intersects_triangle(ray, t0, t1, t2, uv);
-                if (dd < hit.distance) {
-                    hit.distance = dd;
-                    hit.uv = uv;
-                    hit.primitive_index = primitive_index;
-                    hit.instance_index = instance_index;
-                }
-            }
-        } else {
-            go = gb_descend(s, ray, a, b, w[2], w[3], hit.distance, p);
-        }
-        if (go) continue;
-        if (!gb_pop(s, sbase, hit.distance, p)) return;
-    }
-}
+// The same walk with the TLAS and BLAS steps in one loop (as traverse_top): each iteration
+// visits one wide entry of the lane's current level, so a wave's lanes do not wait for each
+// other's BLAS walks.  Identical visits, pushes, pops and hit updates per lane.
 HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = nullptr)
 {
     Hit hit;
@@ -899,27 +869,58 @@ HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = 
     GbStack s;
     s.sp = 0;
     s.lds = lds_stack;
-    uint32_t p = 0u;
+    uint32_t p = 0u;          // subtree start of the current level (mesh-local in a BLAS)
+    bool in_bottom = false;
+    int sbase = 0;            // stack floor of the BLAS walk
+    uint32_t bbase = 0u, prim_offset = 0u, cur = 0u;
+    Ray local = ray;
     for (;;) {
-        const float4* w = sc.tlas_wide + 4u * (size_t)p;
+        const Ray& r = in_bottom ? local : ray;
+        const float4* w = in_bottom ? sc.blas_wide + 4u * (size_t)(bbase + p) : sc.tlas_wide + 4u * (size_t)p;
         const float4 a = w[0], b = w[1];
         const uint32_t entry = __float_as_uint(a.w);
         bool go = false;
         if (entry >= HK_BVH_LEAF_FLAG) {
-            if (intersects_aabb(ray, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance) {
-                const uint32_t instance_index = entry - HK_BVH_LEAF_FLAG;
-                const hk_instance& in = sc.instances[instance_index];
-                Ray r;
-                r.origin = world_to_local_point(in, ray.origin);
-                r.direction = world_to_local_dir(in, ray.direction);
-                r.inv_direction = inv(r.direction);
-                closest_bottom_ordered(sc, s, hit, r, in, instance_index);
+            if (intersects_aabb(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance) {
+                if (in_bottom) {
+                    const uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
+                    f3 t0, t1, t2;
+                    load_triangle(sc.primitives, primitive_index, t0, t1, t2);
+                    f2 uv;
+                    const float dd = intersects_triangle(local, t0, t1, t2, uv);
+                    if (dd < hit.distance) {
+                        hit.distance = dd;
+                        hit.uv = uv;
+                        hit.primitive_index = primitive_index;
+                        hit.instance_index = cur;
+                    }
+                } else {
+                    const uint32_t instance_index = entry - HK_BVH_LEAF_FLAG;
+                    const hk_instance& in = sc.instances[instance_index];
+                    if (in.mesh.node[1] != 0u) {  // closest_bottom_ordered of an empty mesh returns at once
+                        local.origin = world_to_local_point(in, ray.origin);
+                        local.direction = world_to_local_dir(in, ray.direction);
+                        local.inv_direction = inv(local.direction);
+                        bbase = in.mesh.node[0];
+                        prim_offset = in.mesh.primitive;
+                        cur = instance_index;
+                        sbase = s.sp;
+                        in_bottom = true;
+                        p = 0u;
+                        go = true;
+                    }
+                }
             }
         } else {
-            go = gb_descend(s, ray, a, b, w[2], w[3], hit.distance, p);
+            go = gb_descend(s, r, a, b, w[2], w[3], hit.distance, p);
         }
-        if (go) continue;
-        if (!gb_pop(s, 0, hit.distance, p)) return hit;
+        if (!go) {
+            if (in_bottom) {
+                go = gb_pop(s, sbase, hit.distance, p);
+                if (!go) in_bottom = false;  // the BLAS walk returned: continue the TLAS walk
+            }
+            if (!go && !gb_pop(s, 0, hit.distance, p)) return hit;
+        }
     }
 }
 

@@ -61,8 +61,11 @@ for n in (1, 2, 4, 8):
         t0 = time.perf_counter()
         for f in range(10, 10 + steps):
             step(f)
+        t_host = time.perf_counter() - t0  # enqueue time (the queue may throttle it)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
+        if "--kernels" in sys.argv and rank == n // 2:
+            print(f"  N={n} host enqueue {t_host / steps * 1e3:.4f} ms/frame", flush=True)
         worst = max(worst, ms)
         if "--kernels" in sys.argv and rank == n // 2:
             r.enable_kernel_timing(True)
