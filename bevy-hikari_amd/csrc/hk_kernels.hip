@@ -20,28 +20,49 @@
 
 namespace hk {
 
-// workgroup tile -> pixel (global coordinates).
-// Traversal kernels keep the raster tile order: workgroups are dealt round-robin over the 8
-// XCDs, so every XCD works on the same band of the frame at once and per-region cost differences
-// (sky vs. geometry, lit vs. shadowed) are spread evenly (an XCD-stripe order measured 20% slower
-// on cornell 1080p: the XCD holding the expensive stripe finishes last).
-// Spatial reuse measured the same either way and keeps the raster order (its depth window
-// origin is the raster tile). Neighbour-gather kernels (a-trous levels, demodulation) have
-// uniform cost and use the
-// XCD-stripe order (cdna_hip_programming.md T1, bijective form): workgroup L runs on XCD L % 8,
-// and each XCD gets a contiguous range of tiles in raster order, so the taps hit its own L2.
-template <bool XCD_STRIPES = false>
+// workgroup -> 16x16 tile -> pixel (global coordinates).  Tile orders:
+// RASTER: blockIdx in raster order; workgroups are dealt round-robin over the 8 XCDs, so every
+//   XCD works on the same band of the frame at once and per-region cost differences (sky vs.
+//   geometry, lit vs. shadowed) are spread evenly.  The traversal kernels use it (an XCD-stripe
+//   order measured 20% slower on cornell 1080p: the XCD holding the expensive stripe finishes last).
+// XCD_RASTER: the bijective XCD-stripe order (cdna_hip_programming.md T1): workgroup L runs on XCD
+//   L % 8 and each XCD gets a contiguous range of tiles in raster order, so neighbour taps hit its
+//   own L2 (a-trous levels, demodulation, tone mapping).
+// XCD_STRIPS: as XCD_RASTER over tiles enumerated in vertical strips STRIP_TILES wide (raster
+//   inside a strip).  The ~100 workgroups in flight on one XCD then cover a compact 2-D region, so
+//   spatial reuse's 16 neighbour reservoirs (+/- 20 px) stay in that XCD's 4 MiB L2; in raster
+//   order their +/- 20-row window of reservoirs (~7 MB at 1080p) does not fit it.
+enum TileOrder : int { RASTER = 0, XCD_RASTER = 1, XCD_STRIPS = 2 };
+constexpr uint32_t STRIP_TILES = 8;
+template <int ORDER>
+HKD void tile_coords(uint32_t& tx, uint32_t& ty)
+{
+    const uint32_t gx = gridDim.x, gy = gridDim.y;
+    const uint32_t L = blockIdx.x + blockIdx.y * gx;
+    if (ORDER == RASTER) {
+        tx = blockIdx.x;
+        ty = blockIdx.y;
+        return;
+    }
+    const uint32_t n = gx * gy;
+    const uint32_t xcd = L & 7u, i = L >> 3, q = n >> 3, r = n & 7u;
+    const uint32_t tile = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + i;
+    if (ORDER == XCD_RASTER) {
+        tx = tile % gx;
+        ty = tile / gx;
+        return;
+    }
+    const uint32_t per_strip = STRIP_TILES * gy;  // every strip but the last is full width
+    const uint32_t strip = tile / per_strip, k = tile - strip * per_strip;
+    const uint32_t sw = min(STRIP_TILES, gx - strip * STRIP_TILES);
+    ty = k / sw;
+    tx = strip * STRIP_TILES + (k - ty * sw);
+}
+template <int ORDER = RASTER>
 HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
 {
-    const uint32_t gx = gridDim.x;
-    const uint32_t L = blockIdx.x + blockIdx.y * gx;
-    uint32_t tile = L;
-    if (XCD_STRIPES) {
-        const uint32_t n = gridDim.x * gridDim.y;
-        const uint32_t xcd = L & 7u, i = L >> 3, q = n >> 3, r = n & 7u;
-        tile = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + i;
-    }
-    const uint32_t tx = tile % gx, ty = tile / gx;
+    uint32_t tx, ty;
+    tile_coords<ORDER>(tx, ty);
     uint32_t t = threadIdx.x;
     uint32_t w = t >> 6, lane = t & 63u;
     x = (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
@@ -77,12 +98,18 @@ HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, 
 #define HK_INDIRECT_OCC HK_TRACE_OCC
 #endif
 
-// origin (global coordinates) of this workgroup's tile in the raster order
+// origin (global coordinates, contiguous bands) of this workgroup's tile
+template <int ORDER = RASTER>
 HKD void tile_origin(int32_t row0, int32_t& x0, int32_t& y0)
 {
-    x0 = (int32_t)(blockIdx.x * 16u);
-    y0 = row0 + (int32_t)(blockIdx.y * 16u);
+    uint32_t tx, ty;
+    tile_coords<ORDER>(tx, ty);
+    x0 = (int32_t)(tx * 16u);
+    y0 = row0 + (int32_t)(ty * 16u);
 }
+#ifndef HK_SPATIAL_ORDER
+#define HK_SPATIAL_ORDER XCD_STRIPS
+#endif
 
 // ------------------------------------------------------------------ G-buffer
 HKD f3 primary_direction(const ViewArgs& V, float px, float py, const uint32_t* size)
@@ -651,7 +678,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_spatial(FrameArgs A, Chann
     DepthWin W{nullptr, 0, 0};
     if (WINDOW) {
         int32_t x0, y0;
-        tile_origin(A.F.s_row0, x0, y0);
+        tile_origin<HK_SPATIAL_ORDER>(A.F.s_row0, x0, y0);
         W.x0 = x0 - SP_HALO;
         W.y0 = y0 - SP_HALO;
         for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256)
@@ -660,7 +687,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_spatial(FrameArgs A, Chann
         W.lds = win;
     }
     int32_t x, y;
-    if (tile_pixel(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y, W);
+    if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y, W);
 }
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
@@ -694,7 +721,7 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<true>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     f2 uv = coords_to_uv(x, y, F.s);
     f2 duv = jittered_uv(F, uv, 0.5f);
@@ -733,7 +760,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<true>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     constexpr int32_t step = 8 >> LEVEL;
     const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
@@ -824,7 +851,7 @@ __global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<true>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     f4 c = load_rgba16f(T.direct, idx);
     f4 e = load_rgba16f(T.emissive, idx);
