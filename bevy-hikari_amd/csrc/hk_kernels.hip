@@ -33,7 +33,10 @@ namespace hk {
 //   spatial reuse's 16 neighbour reservoirs (+/- 20 px) stay in that XCD's 4 MiB L2; in raster
 //   order their +/- 20-row window of reservoirs (~7 MB at 1080p) does not fit it.
 enum TileOrder : int { RASTER = 0, XCD_RASTER = 1, XCD_STRIPS = 2 };
-constexpr uint32_t STRIP_TILES = 8;
+#ifndef HK_STRIP_TILES
+#define HK_STRIP_TILES 16
+#endif
+constexpr uint32_t STRIP_TILES = HK_STRIP_TILES;
 template <int ORDER>
 HKD void tile_coords(uint32_t& tx, uint32_t& ty)
 {
