@@ -1100,6 +1100,23 @@ void launch_div_check(float d, float r, uint32_t lo, uint32_t hi, unsigned long 
 {
     hipLaunchKernelGGL(k_div_check, dim3(8192), dim3(256), 0, st, d, r, lo, hi, bad);
 }
+// exhaustive check of rcp_exact against the IEEE divide 1 / x over bit patterns [lo, hi), both signs
+__global__ __launch_bounds__(256) void k_rcp_check(uint32_t lo, uint32_t hi, unsigned long long* bad)
+{
+    uint32_t n = 0;
+    for (uint64_t u = (uint64_t)lo + blockIdx.x * 256u + threadIdx.x; u < hi; u += (uint64_t)gridDim.x * 256u) {
+        for (uint32_t sgn = 0; sgn < 2; ++sgn) {
+            const float x = __uint_as_float((uint32_t)u | (sgn << 31));
+            const float a = rcp_exact(x), b = 1.0f / x;
+            if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) n++;
+        }
+    }
+    wave_count(bad, n);
+}
+void launch_rcp_check(uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_rcp_check, dim3(8192), dim3(256), 0, st, lo, hi, bad);
+}
 
 __global__ __launch_bounds__(256) void k_f16(const float* in, uint32_t n, uint16_t* out)
 {

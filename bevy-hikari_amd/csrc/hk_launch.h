@@ -102,6 +102,7 @@ void launch_build_wide(const hk_node* flat, uint32_t n, const uint32_t* node_bas
 void launch_accumulate(const uint2* tone, float4* acc, uint32_t n, int reset, hipStream_t st);
 void launch_resolve(const float4* acc, uint32_t n, float count, uint2* out, hipStream_t st);
 void launch_div_check(float d, float r, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t st);
+void launch_rcp_check(uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t st);
 void launch_f16(const float* in, uint32_t n, uint16_t* out, hipStream_t st);
 void launch_trace(const Scene& sc, const float* rays, const float* max_d, const float* early_d, const uint32_t* excl,
                   uint32_t n, uint32_t* hits, unsigned long long* top, hipStream_t st);

@@ -1282,4 +1282,25 @@ int hk_selftest_div(hk_ctx* c, float divisor, uint32_t lo, uint32_t hi, uint64_t
     return HK_OK;
 }
 
+int hk_selftest_rcp(hk_ctx* c, uint32_t lo, uint32_t hi, uint64_t* mismatches)
+{
+    if (!c || !mismatches || lo > hi) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, nullptr);
+    unsigned long long* d_bad = nullptr;
+    const size_t bytes = (size_t)COUNTER_SHARDS * COUNTER_STRIDE * 8;
+    HK_HIP(c, hipMalloc(&d_bad, bytes));
+    HK_HIP(c, hipMemsetAsync(d_bad, 0, bytes, st));
+    launch_rcp_check(lo, hi, d_bad, st);
+    HK_HIP(c, hipGetLastError());
+    std::vector<unsigned long long> h(bytes / 8);
+    HK_HIP(c, hipMemcpyAsync(h.data(), d_bad, bytes, hipMemcpyDeviceToHost, st));
+    HK_HIP(c, hipStreamSynchronize(st));
+    release(d_bad);
+    uint64_t total = 0;
+    for (size_t k = 0; k < h.size(); k += COUNTER_STRIDE) total += h[k];
+    *mismatches = total;
+    return HK_OK;
+}
+
 }  // extern "C"

@@ -162,6 +162,7 @@ def lib() -> C.CDLL:
         "hk_trace": (i32, [vp, vp, vp, vp, vp, u32, vp, i32, vp]),
         "hk_selftest_f16": (i32, [vp, vp, u32, vp]),
         "hk_selftest_div": (i32, [vp, C.c_float, u32, u32, C.POINTER(C.c_uint64)]),
+        "hk_selftest_rcp": (i32, [vp, u32, u32, C.POINTER(C.c_uint64)]),
         "hks_create": (vp, []),
         "hks_destroy": (None, [vp]),
         "hks_last_error": (C.c_char_p, [vp]),
@@ -185,7 +186,7 @@ EXPORTED_SYMBOLS = [
     "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
-    "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",
+    "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hk_selftest_rcp", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",
     "hks_add_instance", "hks_build", "hks_get_desc",
 ]
 

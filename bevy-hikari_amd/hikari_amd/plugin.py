@@ -188,6 +188,12 @@ class HikariRenderer:
                                           None), "hk_trace")
         return hits
 
+    def selftest_rcp(self, lo: int, hi: int) -> int:
+        """f32 bit patterns in [lo, hi) (both signs) where the kernels' rcp_exact(x) != 1 / x."""
+        n = C.c_uint64()
+        _check(self.ctx, self._L.hk_selftest_rcp(self.ctx, lo, hi, C.byref(n)), "hk_selftest_rcp")
+        return n.value
+
     def selftest_div(self, divisor: float, lo: int, hi: int) -> int:
         """Mismatches of the kernels' division by a frame dimension against IEEE x / divisor."""
         n = C.c_uint64()

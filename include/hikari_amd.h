@@ -280,6 +280,9 @@ int hk_selftest_f16(hk_ctx* ctx, const float* in, uint32_t n, uint16_t* out);
 /* ---- self-test of the kernels' division by a frame dimension (div_by, hk_device.h): counts the
  * f32 bit patterns x in [lo, hi) (both signs) where div_by(x, divisor) != x / divisor */
 int hk_selftest_div(hk_ctx* ctx, float divisor, uint32_t lo, uint32_t hi, uint64_t* mismatches);
+/* ---- self-test of the kernels' reciprocal (rcp_exact, hk_device.h): counts the f32 bit patterns
+ * x in [lo, hi) (both signs) where rcp_exact(x) != 1 / x (IEEE) */
+int hk_selftest_rcp(hk_ctx* ctx, uint32_t lo, uint32_t hi, uint64_t* mismatches);
 
 #ifdef __cplusplus
 }

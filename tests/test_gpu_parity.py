@@ -342,6 +342,14 @@ def test_fast_division_by_frame_size_is_exact():
     assert not any(bad.values()), {d: n for d, n in bad.items() if n}
 
 
+def test_fast_reciprocal_is_exact():
+    """rcp_exact (hk_device.h) returns the IEEE quotient 1 / x bit for bit for every f32 x
+    (all 2^32 patterns: zeros, denormals, infinities and NaNs included)."""
+    from hikari_amd import HikariRenderer
+    r = HikariRenderer(0)
+    assert r.selftest_rcp(0, 0x80000000) == 0
+
+
 def _moved(scene_fn, seed):
     """The scene with every instance moved/rotated/scaled by a seeded transform."""
     from hikari_amd import examples
