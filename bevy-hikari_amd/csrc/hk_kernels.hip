@@ -1073,6 +1073,44 @@ void launch_build_wide(const hk_node* flat, uint32_t n, const uint32_t* node_bas
                               wide);
 }
 
+// Leaf collapse of the device node copies for the light-pass walks.  bvh 0.7.1 flattens a leaf
+// child into a child-box node p (the BVH's child AABB; entry p+1, exit q) followed by the leaf
+// node p+1 (payload, exit q).  The reference tests p's box, then at p+1 the recomputed triangle /
+// instance box (light.wgsl:411-413, 456-457) with the same ray and the same hit distance (nothing
+// changes between the two visits).  Where the two boxes are bitwise identical the second test
+// repeats the first, so p can take the leaf's payload (entry = LEAF | payload, same exit): one
+// node visit per leaf instead of two, the same tests and results.  Two passes (decide, write) so
+// no thread reads a node another thread rewrites.  The G-buffer wide layout is built before this.
+__global__ __launch_bounds__(256) void k_collapse_decide(const hk_node* nodes, uint32_t n, const uint32_t* node_base,
+                                                         const uint32_t* node_count, uint32_t* new_entry)
+{
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n) return;
+    const hk_node nd = nodes[p];
+    new_entry[p] = nd.entry_index;
+    const uint32_t base = node_base ? node_base[p] : 0u, count = node_count ? node_count[p] : n;
+    if (base == HK_U32_MAX || nd.entry_index >= HK_BVH_LEAF_FLAG || nd.entry_index >= count) return;
+    const hk_node lf = nodes[base + nd.entry_index];
+    if (lf.entry_index < HK_BVH_LEAF_FLAG || lf.exit_index != nd.exit_index) return;
+    for (int k = 0; k < 3; ++k)
+        if (__float_as_uint(lf.min[k]) != __float_as_uint(nd.min[k]) || __float_as_uint(lf.max[k]) != __float_as_uint(nd.max[k]))
+            return;
+    new_entry[p] = lf.entry_index;
+}
+__global__ __launch_bounds__(256) void k_collapse_write(hk_node* nodes, uint32_t n, const uint32_t* new_entry)
+{
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p < n) nodes[p].entry_index = new_entry[p];
+}
+void launch_collapse_leaves(hk_node* nodes, uint32_t n, const uint32_t* node_base, const uint32_t* node_count,
+                            uint32_t* scratch, hipStream_t st)
+{
+    if (!n) return;
+    const dim3 g((n + 255u) / 256u);
+    hipLaunchKernelGGL(k_collapse_decide, g, dim3(256), 0, st, nodes, n, node_base, node_count, scratch);
+    hipLaunchKernelGGL(k_collapse_write, g, dim3(256), 0, st, nodes, n, scratch);
+}
+
 void launch_fill_leaves(hk_node* blas, uint32_t n_blas, const uint32_t* prim_offset, const hk_primitive* prims,
                         hk_node* tlas, uint32_t n_tlas, const hk_instance* inst, uint32_t n_inst, hipStream_t st)
 {

@@ -95,6 +95,8 @@ void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit,
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st);
 void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st);
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st);
+void launch_collapse_leaves(hk_node* nodes, uint32_t n, const uint32_t* node_base, const uint32_t* node_count,
+                            uint32_t* scratch, hipStream_t st);
 void launch_fill_leaves(hk_node* blas, uint32_t n_blas, const uint32_t* prim_offset, const hk_primitive* prims,
                         hk_node* tlas, uint32_t n_tlas, const hk_instance* inst, uint32_t n_inst, hipStream_t st);
 void launch_build_wide(const hk_node* flat, uint32_t n, const uint32_t* node_base, const uint32_t* node_count,

@@ -41,6 +41,8 @@ struct hk_ctx {
     // scene
     void* buf[9] = {};
     uint32_t count[9] = {};
+    hk_node* walk_nodes[2] = {nullptr, nullptr};  // BLAS / TLAS copies of the light walks (leaf-collapsed)
+    uint32_t* collapse_scratch = nullptr;
     float4* blas_wide = nullptr;  // G-buffer traversal layout (k_build_wide)
     float4* tlas_wide = nullptr;
     uint32_t gb_stack_need = 0;   // TLAS + BLAS subtree depth bound of closest_hit_ordered
@@ -221,10 +223,10 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     std::memset(&A, 0, sizeof(A));
     A.sc.vertices = (const hk_vertex*)c->buf[0];
     A.sc.primitives = (const hk_primitive*)c->buf[1];
-    A.sc.asset_nodes = (const hk_node*)c->buf[2];
+    A.sc.asset_nodes = c->walk_nodes[0];  // leaf-collapsed copies (launch_collapse_leaves)
     A.sc.alias_table = (const hk_alias_entry*)c->buf[3];
     A.sc.instances = (const hk_instance*)c->buf[4];
-    A.sc.instance_nodes = (const hk_node*)c->buf[5];
+    A.sc.instance_nodes = c->walk_nodes[1];
     A.sc.materials = (const hk_material*)c->buf[6];
     A.sc.emissive_nodes = (const hk_node*)c->buf[7];
     A.sc.emissives = (const hk_emissive*)c->buf[8];
@@ -402,6 +404,9 @@ void hk_destroy(hk_ctx* c)
     for (int i = 0; i < 9; ++i) release(c->buf[i]);
     release(c->blas_wide);
     release(c->tlas_wide);
+    release(c->walk_nodes[0]);
+    release(c->walk_nodes[1]);
+    release(c->collapse_scratch);
     release(c->dyn_scratch);
     release(c->tex_desc);
     release(c->texels);
@@ -499,11 +504,28 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
     HK_HIP(c, hipGetLastError());
     release(c->blas_wide);
     release(c->tlas_wide);
+    release(c->walk_nodes[0]);
+    release(c->walk_nodes[1]);
+    release(c->collapse_scratch);
     HK_HIP(c, hipMalloc(&c->blas_wide, (size_t)(n_blas ? n_blas : 1) * 64));
     HK_HIP(c, hipMalloc(&c->tlas_wide, (size_t)(n_tlas ? n_tlas : 1) * 64));
     launch_build_wide((const hk_node*)c->buf[2], n_blas, d_aux + n_blas, d_aux + 2 * (size_t)n_blas, c->blas_wide,
                       c->stream);
     launch_build_wide((const hk_node*)c->buf[5], n_tlas, nullptr, nullptr, c->tlas_wide, c->stream);
+    // the light walks' node copies, leaf-collapsed (k_collapse_decide); the arrays above stay as
+    // uploaded (hk_read_scene_array, the wide layout and hk_update_instances read them)
+    HK_HIP(c, hipMalloc(&c->walk_nodes[0], (size_t)(n_blas ? n_blas : 1) * sizeof(hk_node)));
+    HK_HIP(c, hipMalloc(&c->walk_nodes[1], (size_t)(n_tlas ? n_tlas : 1) * sizeof(hk_node)));
+    HK_HIP(c, hipMalloc(&c->collapse_scratch, (size_t)std::max<uint32_t>(1u, std::max(n_blas, n_tlas)) * 4));
+    HK_HIP(c, hipMemcpyAsync(c->walk_nodes[0], c->buf[2], (size_t)n_blas * sizeof(hk_node), hipMemcpyDeviceToDevice,
+                             c->stream));
+    HK_HIP(c, hipMemcpyAsync(c->walk_nodes[1], c->buf[5], (size_t)n_tlas * sizeof(hk_node), hipMemcpyDeviceToDevice,
+                             c->stream));
+    if (!getenv("HK_NO_COLLAPSE")) {
+        launch_collapse_leaves(c->walk_nodes[0], n_blas, d_aux + n_blas, d_aux + 2 * (size_t)n_blas, c->collapse_scratch,
+                               c->stream);
+        launch_collapse_leaves(c->walk_nodes[1], n_tlas, nullptr, nullptr, c->collapse_scratch, c->stream);
+    }
     HK_HIP(c, hipGetLastError());
     HK_HIP(c, hipStreamSynchronize(c->stream));
     release(d_aux);
@@ -568,6 +590,10 @@ int hk_update_instances(hk_ctx* c, const float* models, const float* local_aabbs
         launch_fill_leaves(nullptr, 0, nullptr, nullptr, (hk_node*)c->buf[5], c->count[5], (const hk_instance*)c->buf[4],
                            n, st);
         launch_build_wide((const hk_node*)c->buf[5], c->count[5], nullptr, nullptr, c->tlas_wide, st);
+        (void)hipMemcpyAsync(c->walk_nodes[1], c->buf[5], (size_t)c->count[5] * sizeof(hk_node), hipMemcpyDeviceToDevice,
+                             st);
+        if (!getenv("HK_NO_COLLAPSE"))
+            launch_collapse_leaves(c->walk_nodes[1], c->count[5], nullptr, nullptr, c->collapse_scratch, st);
     });
     HK_HIP(c, hipGetLastError());
     uint32_t flags[2] = {0, 0};
