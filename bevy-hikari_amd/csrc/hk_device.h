@@ -800,9 +800,11 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
 // Ordered closest-hit traversal, the build's own primary-visibility rule (the reference
 // rasterises the G-buffer); defined in oracle/hk_oracle.c (closest_hit_ordered) and reproduced
 // here step for step.  Wide entry of a subtree start p (4 x float4, one 64-byte line):
-//   inner: (left box min, left subtree start), (left box max, right subtree start),
-//          (right box min, -), (right box max, -)      [starts mesh-local for BLAS]
-//   leaf:  (leaf box min, entry = payload | LEAF), (leaf box max, -)
+//   inner: (left box min, left target), (left box max, right target),
+//          (right box min, -), (right box max, -)      [targets mesh-local for BLAS]
+//   leaf:  (leaf box min, entry = payload | LEAF), (leaf box max, U32_MAX)
+// A target is the child's subtree start, or LEAF | payload when the child is a single leaf whose
+// box equals the child box (k_build_wide): its box test is then the descent's / pop's comparison.
 // Leaf boxes are the triangle's / instance's box, as the reference walk tests them.
 constexpr int GB_STACK = 64;
 // Stack entries (node, entry distance): the first GB_STACK_LDS live in the workgroup's LDS
@@ -894,12 +896,23 @@ HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = 
     Ray local = ray;
     for (;;) {
         const Ray& r = in_bottom ? local : ray;
-        const float4* w = in_bottom ? sc.blas_wide + 4u * (size_t)(bbase + p) : sc.tlas_wide + 4u * (size_t)p;
-        const float4 a = w[0], b = w[1];
-        const uint32_t entry = __float_as_uint(a.w);
-        bool go = false;
+        // p: a wide entry, or (LEAF | payload) for a leaf child whose box is its parent entry's child
+        // box (k_build_wide): that box test already passed, at the descent or at the pop
+        uint32_t entry = p;
+        bool pass = true, go = false;
+        float4 a, b;
+        const float4* w = nullptr;
+        if (p < HK_BVH_LEAF_FLAG) {
+            w = in_bottom ? sc.blas_wide + 4u * (size_t)(bbase + p) : sc.tlas_wide + 4u * (size_t)p;
+            a = w[0];
+            b = w[1];
+            // a leaf entry (single-leaf tree root) has w[1].w == U32_MAX; an inner entry's a.w is its
+            // left target, which may itself be (LEAF | payload)
+            entry = __float_as_uint(b.w) == HK_U32_MAX ? __float_as_uint(a.w) : 0u;
+            if (entry >= HK_BVH_LEAF_FLAG) pass = intersects_aabb(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance;
+        }
         if (entry >= HK_BVH_LEAF_FLAG) {
-            if (intersects_aabb(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z)) < hit.distance) {
+            if (pass) {
                 if (in_bottom) {
                     const uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
                     f3 t0, t1, t2;

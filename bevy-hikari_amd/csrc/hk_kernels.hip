@@ -1052,17 +1052,31 @@ __global__ __launch_bounds__(256) void k_build_wide(const hk_node* flat, uint32_
     float4* w = wide + 4u * (size_t)p;
     const hk_node& f = flat[p];
     const uint32_t base = node_base ? node_base[p] : 0u, count = node_count ? node_count[p] : n;
+    // leaf entry: (box min, payload | LEAF), (box max, U32_MAX); inner: see below (w[1].w != U32_MAX)
     w[0] = make_float4(f.min[0], f.min[1], f.min[2], __uint_as_float(f.entry_index));
-    w[1] = make_float4(f.max[0], f.max[1], f.max[2], 0.0f);
+    w[1] = make_float4(f.max[0], f.max[1], f.max[2], __uint_as_float(HK_U32_MAX));
     w[2] = make_float4(0, 0, 0, 0);
     w[3] = make_float4(0, 0, 0, 0);
     if (f.entry_index >= HK_BVH_LEAF_FLAG || base == HK_U32_MAX) return;
-    // inner subtree starting at p: left box node p (subtree p+1), right box node q (subtree q+1)
+    // inner subtree starting at p: left box node p (subtree p+1), right box node q (subtree q+1).
+    // A child subtree that is a single leaf whose box equals the child box (bitwise) is stored as
+    // its payload (LEAF | payload): the walk's descent / pop comparison already is that leaf's
+    // box test, so the leaf entry is not loaded.
     const uint32_t local = p - base, q_local = f.exit_index;
     if (q_local >= count) return;  // p is a right-child box node, never a subtree start
     const hk_node& g = flat[base + q_local];
-    w[0].w = __uint_as_float(local + 1u);
-    w[1].w = __uint_as_float(q_local + 1u);
+    auto target = [&](const hk_node& child, uint32_t start) -> uint32_t {
+        if (start >= count) return start;
+        const hk_node& lf = flat[base + start];
+        if (lf.entry_index < HK_BVH_LEAF_FLAG) return start;
+        for (int k = 0; k < 3; ++k)
+            if (__float_as_uint(lf.min[k]) != __float_as_uint(child.min[k]) ||
+                __float_as_uint(lf.max[k]) != __float_as_uint(child.max[k]))
+                return start;
+        return lf.entry_index;
+    };
+    w[0].w = __uint_as_float(target(f, local + 1u));
+    w[1].w = __uint_as_float(target(g, q_local + 1u));
     w[2] = make_float4(g.min[0], g.min[1], g.min[2], 0.0f);
     w[3] = make_float4(g.max[0], g.max[1], g.max[2], 0.0f);
 }
