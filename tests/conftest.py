@@ -5,7 +5,7 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
-for p in (ROOT / "bevy-hikari_amd", ROOT / "oracle", ROOT / "tests"):
+for p in (ROOT, ROOT / "bevy-hikari_amd", ROOT / "oracle", ROOT / "tests"):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
 

@@ -76,6 +76,40 @@ def test_cornell_frames_bit_exact(size, lds_mode):
     assert r.counters() == o.counters()
 
 
+@pytest.mark.parametrize("config,frames", [("cornell-1080p-nee", 4), ("scene-1080p-full", 2), ("city-4k", 2)])
+def test_full_size_bench_workloads_bit_exact(config, frames):
+    """The bench workloads themselves (BASELINE configs 2-4 at 1920x1080 and 3840x2160): every output plane
+    of every frame, all reservoir buffers of the last frame and the ray counters bit-exact."""
+    import bench
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    cfg = bench.CONFIGS[config]
+    w, h = cfg["width"], cfg["height"]
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
+    scene, cam, lights, r, o = _setup(w, h, st, cfg["scene"])
+    s = st.to_c()
+    errors = []
+    for f in range(frames):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        for oid in OUTPUTS:
+            m = mismatch_report(canon_plane(oid, r.output(oid)), canon_plane(oid, o.output(oid)), f"frame {f} output {oid}")
+            if m:
+                errors.append(m)
+        if errors:
+            break
+    for rid in range(10):
+        g = r.reservoirs(rid)
+        m = mismatch_report(canon_reservoirs(g), canon_reservoirs(o.reservoirs(rid)[: len(g)]), f"reservoir {rid}")
+        if m:
+            errors.append(m)
+    assert not errors, "\n".join(errors[:20])
+    assert r.counters() == o.counters()
+
+
 def test_trace_matches_oracle():
     from hikari_amd import HikariSettings, Upscale
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
