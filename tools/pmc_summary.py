@@ -26,7 +26,8 @@ SHORT = {  # mangled and demangled spellings
     "k_spatialILb1": "emissive_spatial_reuse", "k_spatial<true": "emissive_spatial_reuse",
     "k_demod3": "demodulation", "k_denoise3": "denoise", "k_tone": "tone_mapping", "k_trace": "trace",
     "k_f16": "f16_selftest", "k_build_wide": "scene_build_wide", "k_fill_blas_leaves": "scene_fill_leaves",
-    "k_fill_tlas_leaves": "scene_fill_leaves",
+    "k_fill_tlas_leaves": "scene_fill_leaves", "k_collapse_decide": "scene_collapse_leaves",
+    "k_collapse_write": "scene_collapse_leaves",
 }
 
 
