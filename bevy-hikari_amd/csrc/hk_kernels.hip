@@ -27,11 +27,12 @@ namespace hk {
 //   order measured 20% slower on cornell 1080p: the XCD holding the expensive stripe finishes last).
 // XCD_RASTER: the bijective XCD-stripe order (cdna_hip_programming.md T1): workgroup L runs on XCD
 //   L % 8 and each XCD gets a contiguous range of tiles in raster order, so neighbour taps hit its
-//   own L2 (a-trous levels, demodulation, tone mapping).
+//   own L2 (demodulation, tone mapping).
 // XCD_STRIPS: as XCD_RASTER over tiles enumerated in vertical strips STRIP_TILES wide (raster
 //   inside a strip).  The ~100 workgroups in flight on one XCD then cover a compact 2-D region, so
 //   spatial reuse's 16 neighbour reservoirs (+/- 20 px) stay in that XCD's 4 MiB L2; in raster
-//   order their +/- 20-row window of reservoirs (~7 MB at 1080p) does not fit it.
+//   order their +/- 20-row window of reservoirs (~7 MB at 1080p) does not fit it.  The a-trous
+//   levels use it too (city 4K: 0.529 -> 0.436 ms per level).
 enum TileOrder : int { RASTER = 0, XCD_RASTER = 1, XCD_STRIPS = 2 };
 #ifndef HK_STRIP_TILES
 #define HK_STRIP_TILES 16
@@ -112,6 +113,9 @@ HKD void tile_origin(int32_t row0, int32_t& x0, int32_t& y0)
 }
 #ifndef HK_SPATIAL_ORDER
 #define HK_SPATIAL_ORDER XCD_STRIPS
+#endif
+#ifndef HK_DENOISE_ORDER  // the a-trous levels (taps up to 8 px away): city 4K 0.529 -> 0.436 ms per level
+#define HK_DENOISE_ORDER XCD_STRIPS
 #endif
 
 // ------------------------------------------------------------------ G-buffer
@@ -763,7 +767,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<HK_DENOISE_ORDER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     constexpr int32_t step = 8 >> LEVEL;
     const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
