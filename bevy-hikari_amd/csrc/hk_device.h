@@ -810,14 +810,17 @@ constexpr int GB_STACK = 64;
 // Stack entries (node, entry distance): the first GB_STACK_LDS live in the workgroup's LDS
 // (entry-major, one uint2 per thread per level: conflict-free), deeper ones in private scratch.
 constexpr int GB_STACK_LDS = 16;
-struct GbStack {
+// SHALLOW: the scene's stack bound fits the LDS levels (hk_runtime gb_stack_need), so there is no
+// private overflow array (no scratch allocation for the kernel's waves)
+template <bool SHALLOW>
+struct GbStackT {
     uint2* lds;  // [GB_STACK_LDS][blockDim.x], or null
-    uint32_t node[GB_STACK - GB_STACK_LDS];
-    float t[GB_STACK - GB_STACK_LDS];
+    uint32_t node[SHALLOW ? 1 : GB_STACK - GB_STACK_LDS];
+    float t[SHALLOW ? 1 : GB_STACK - GB_STACK_LDS];
     int sp;
     HKD void push(uint32_t n, float tt)
     {
-        if (lds && sp < GB_STACK_LDS) lds[sp * 256 + threadIdx.x] = make_uint2(n, __float_as_uint(tt));
+        if (SHALLOW || (lds && sp < GB_STACK_LDS)) lds[sp * 256 + threadIdx.x] = make_uint2(n, __float_as_uint(tt));
         else {
             const int k = lds ? sp - GB_STACK_LDS : sp;
             node[k] = n;
@@ -827,7 +830,7 @@ struct GbStack {
     }
     HKD void top(uint32_t& n, float& tt) const
     {
-        if (lds && sp < GB_STACK_LDS) {
+        if (SHALLOW || (lds && sp < GB_STACK_LDS)) {
             const uint2 e = lds[sp * 256 + threadIdx.x];
             n = e.x;
             tt = __uint_as_float(e.y);
@@ -838,6 +841,7 @@ struct GbStack {
         }
     }
 };
+template <class GbStack>
 HKD bool gb_pop(GbStack& s, int base, float best, uint32_t& n)
 {
     while (s.sp > base) {
@@ -853,6 +857,7 @@ HKD bool gb_pop(GbStack& s, int base, float best, uint32_t& n)
     return false;
 }
 // one inner step: enter the nearer passing child, push the farther; false if neither passes
+template <class GbStack>
 HKD bool gb_descend(GbStack& s, const Ray& ray, float4 a, float4 b, float4 c, float4 d, float best, uint32_t& p)
 {
     const float tl = intersects_aabb(ray, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
@@ -878,6 +883,7 @@ HKD bool gb_descend(GbStack& s, const Ray& ray, float4 a, float4 b, float4 c, fl
 // The same walk with the TLAS and BLAS steps in one loop (as traverse_top): each iteration
 // visits one wide entry of the lane's current level, so a wave's lanes do not wait for each
 // other's BLAS walks.  Identical visits, pushes, pops and hit updates per lane.
+template <bool SHALLOW = false>
 HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = nullptr)
 {
     Hit hit;
@@ -886,7 +892,7 @@ HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = 
     hit.instance_index = HK_U32_MAX;
     hit.primitive_index = HK_U32_MAX;
     if (sc.n_instance_nodes == 0u) return hit;
-    GbStack s;
+    GbStackT<SHALLOW> s;
     s.sp = 0;
     s.lds = lds_stack;
     uint32_t p = 0u;          // subtree start of the current level (mesh-local in a BLAS)

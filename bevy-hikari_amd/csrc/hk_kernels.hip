@@ -114,6 +114,9 @@ HKD void tile_origin(int32_t row0, int32_t& x0, int32_t& y0)
 #ifndef HK_SPATIAL_ORDER
 #define HK_SPATIAL_ORDER XCD_STRIPS
 #endif
+#ifndef HK_TRACE_ORDER  // G-buffer and light-pass kernels
+#define HK_TRACE_ORDER RASTER
+#endif
 #ifndef HK_DENOISE_ORDER  // the a-trous levels (taps up to 8 px away): city 4K 0.529 -> 0.436 ms per level
 #define HK_DENOISE_ORDER XCD_STRIPS
 #endif
@@ -150,7 +153,7 @@ HKD f4 albedo_of(const Frame& F, const Scene& sc, f4 pd, uint32_t packed_normal,
 }
 
 // albedo != null: the frame's full_screen_albedo is written here too (hk_render_frame skips it)
-template <bool LDS>
+template <bool LDS, bool SHALLOW>
 __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewArgs V, uint2* albedo)
 {
     // the traversal stack's first GB_STACK_LDS levels (32 KiB; the scene-staged variant keeps the
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
     if constexpr (LDS) sc = stage_scene<PLAN_GBUFFER>(A.sc, hk_lds_scene);
     else sc = A.sc;
     int32_t x, y;
-    bool active = tile_pixel(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
+    bool active = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
     uint32_t n_primary = 0;
     if (active) {
         n_primary = 1;
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
         ray.origin = ld3(V.world_position);
         ray.direction = primary_direction(V, (float)x + 0.5f, (float)y + 0.5f, A.F.S);
         ray.inv_direction = inv(ray.direction);
-        Hit hit = closest_hit_ordered(sc, ray, LDS ? nullptr : gb_lds_stack);
+        Hit hit = closest_hit_ordered<SHALLOW && !LDS>(sc, ray, LDS ? nullptr : gb_lds_stack);
         if (hit.instance_index == HK_U32_MAX) {
             A.G.position[idx] = make_float4(0, 0, 0, 0);
             A.G.normal[idx] = 0u;
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
 __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
 {
     int32_t x, y;
-    if (!tile_pixel(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
+    if (!tile_pixel<HK_TRACE_ORDER>(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
     const int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
     const f4 pd = load_position(A.F, A.G, x, y);
     if (pd.w < HK_F32_EPSILON) {
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_body<EMISSIVE_LIT, RENDER_EMISSIVE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -534,7 +537,7 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -919,11 +922,14 @@ static uint32_t lds_plan_bytes(const FrameArgs& A, int plan, bool preferred)
     return b <= LDS_SCENE_MAX ? b : 0u;
 }
 
-void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, hipStream_t st)
+void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32_t stack_need, hipStream_t st)
 {
     const uint32_t lds = lds_plan_bytes(A, PLAN_GBUFFER, false);
-    if (lds) hipLaunchKernelGGL(k_gbuffer<true>, tiles(A.F.S[0], A.F.S_rows), dim3(256), lds, st, A, V, albedo);
-    else hipLaunchKernelGGL(k_gbuffer<false>, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, V, albedo);
+    const dim3 g = tiles(A.F.S[0], A.F.S_rows);
+    if (lds) hipLaunchKernelGGL((k_gbuffer<true, false>), g, dim3(256), lds, st, A, V, albedo);
+    else if (stack_need <= (uint32_t)GB_STACK_LDS && !getenv("HK_GB_DEEP"))
+        hipLaunchKernelGGL((k_gbuffer<false, true>), g, dim3(256), 0, st, A, V, albedo);
+    else hipLaunchKernelGGL((k_gbuffer<false, false>), g, dim3(256), 0, st, A, V, albedo);
 }
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st)
 {

@@ -822,7 +822,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     std::memcpy(V.inverse_view_proj, in->view.inverse_view_proj, sizeof(V.inverse_view_proj));
     // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
     // hk_render_frame runs it on its own only for host-supplied G-buffers
-    timed(c, "gbuffer", st, [&] { launch_gbuffer(A, V, c->albedo, st); });
+    timed(c, "gbuffer", st, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, st); });
     c->albedo_fresh = true;
     HK_HIP(c, hipGetLastError());
     return HK_OK;
