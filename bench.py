@@ -47,6 +47,7 @@ BYTES_PER_PIXEL = {
     "full_screen_albedo": 52,        # reads 44 B of G-buffer, writes RGBA16F
     "direct_lit": 184,               # G 44 + reservoir read 64 + write 64 + variance 4 + render 8
     "direct_emissive": 184,
+    "direct_lit_emissive": 368,      # both passes in one launch (k_direct_fused)
     "indirect_lit_ambient": 184,
     "indirect_multiple_bounces": 184,
     "indirect_spatial_reuse": 244,   # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8

@@ -370,6 +370,28 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     wave_count(A.cnt.emitter, n_emitter);
 }
 
+// direct_lit then the emissive pass in one launch, each thread running both passes for its pixel
+// in the reference's pass order.  Both passes store into the spatial reservoir pair they share
+// only at their own pixel when the reprojection is the identity (zero velocity at upscale ratio
+// 1: the G-buffer of k_gbuffer), so per-thread program order is the reference's pass order for
+// every stored word; the runtime uses it only then.  One launch and one tail instead of two.
+template <bool LDS>
+__global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A, ChannelArgs C0, ChannelArgs C1)
+{
+    Scene sc;
+    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+    else sc = A.sc;
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
+        direct_body<false, true>(A, sc, C0, x, y, n_top, n_emitter);
+        direct_body<true, false>(A, sc, C1, x, y, n_top, n_emitter);
+    }
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
 // ------------------------------------------------------------------ indirect_lit_ambient (light.wgsl:1263-1498)
 template <bool MULTI>
 HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top, uint32_t& n_emitter)
@@ -946,6 +968,13 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
         if (lds) hipLaunchKernelGGL((k_direct<false, true, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_direct<false, true, false>), g, dim3(256), 0, st, A, C);
     }
+}
+void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, hipStream_t st)
+{
+    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
+    if (lds) hipLaunchKernelGGL(k_direct_fused<true>, g, dim3(256), lds, st, A, C0, C1);
+    else hipLaunchKernelGGL(k_direct_fused<false>, g, dim3(256), 0, st, A, C0, C1);
 }
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st)
 {
