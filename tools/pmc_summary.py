@@ -18,6 +18,7 @@ from pathlib import Path
 
 SHORT = {  # mangled and demangled spellings
     "k_gbuffer": "gbuffer", "k_albedo": "full_screen_albedo",
+    "k_direct_fused": "direct_lit_emissive",
     "k_directILb0ELb1": "direct_lit", "k_direct<false, true": "direct_lit",
     "k_directILb1ELb0": "direct_emissive", "k_direct<true, false": "direct_emissive",
     "k_indirectILb0": "indirect_lit_ambient", "k_indirect<false": "indirect_lit_ambient",
