@@ -110,6 +110,31 @@ def test_full_size_bench_workloads_bit_exact(config, frames):
     assert r.counters() == o.counters()
 
 
+def test_fallback_paths_bit_exact(monkeypatch):
+    """The paths the defaults switch off stay exact: one stream (no channel fork), walk nodes
+    without leaf collapse, the G-buffer stack with its scratch overflow levels."""
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    for k, v in (("HK_CHANNEL_STREAMS", "0"), ("HK_NO_COLLAPSE", "1"), ("HK_GB_DEEP", "1")):
+        monkeypatch.setenv(k, v)
+    w, h = 64, 48
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
+    scene, cam, lights, r, o = _setup(w, h, st)
+    s = st.to_c()
+    errors = []
+    for f in range(4):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        _compare_frame(r, o, f, errors)
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
+    assert r.counters() == o.counters()
+
+
 def test_trace_matches_oracle():
     from hikari_amd import HikariSettings, Upscale
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
