@@ -637,12 +637,64 @@ HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& 
     c = mk3(z.x, z.y, z.z);
 }
 
+#ifndef HK_TRAVERSE_PAIRSTEP
+#define HK_TRAVERSE_PAIRSTEP 1
+#endif
+
 // light.wgsl:400-440 — stackless skip-pointer BLAS walk (reference visit order).
 HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t node_offset, uint32_t node_count,
                          uint32_t prim_offset, float early_distance)
 {
     bool intersected = false;
     uint32_t index = 0u;
+#if HK_TRAVERSE_PAIRSTEP
+    // two visits per iteration as in traverse_top below: a passing inner node p is followed by
+    // p + 1 (its subtree start), tested with the same hit distance in the same iteration
+    const hk_node* nodes = sc.asset_nodes + node_offset;
+    while (index < node_count) {
+        f3 mn, mx, mn2, mx2;
+        uint32_t entry, exit, entry2, exit2;
+        const uint32_t index2 = index + 1u < node_count ? index + 1u : index;
+        load_node(nodes, index, mn, entry, mx, exit);
+        load_node(nodes, index2, mn2, entry2, mx2, exit2);
+        const bool pass = intersects_aabb(ray, mn, mx) < hit.distance;
+        const bool pass2 = intersects_aabb(ray, mn2, mx2) < hit.distance;
+        bool leaf_pass = false;
+        uint32_t leaf_entry = entry, next;
+        if (entry < HK_BVH_LEAF_FLAG) {
+            if (pass) {
+                if (entry2 < HK_BVH_LEAF_FLAG) {
+                    next = pass2 ? entry2 : exit2;
+                } else {
+                    leaf_pass = pass2;
+                    leaf_entry = entry2;
+                    next = exit2;
+                }
+            } else {
+                next = exit;
+            }
+        } else {
+            leaf_pass = pass;
+            next = exit;
+        }
+        if (leaf_pass) {
+            uint32_t primitive_index = prim_offset + leaf_entry - HK_BVH_LEAF_FLAG;
+            f3 a, b, c;
+            load_triangle(sc.primitives, primitive_index, a, b, c);
+            f2 uv;
+            float d = intersects_triangle(ray, a, b, c, uv);
+            if (d < hit.distance) {
+                hit.distance = d;
+                hit.uv = uv;
+                hit.primitive_index = primitive_index;
+                intersected = true;
+                if (d < early_distance) return intersected;
+            }
+        }
+        index = next;
+    }
+    return intersected;
+#endif
     while (index < node_count) {
         f3 mn, mx;
         uint32_t entry, exit;
@@ -716,6 +768,105 @@ HKD f3 local_to_world_normal(const hk_instance& in, f3 n)
 // lanes wait.  Here all lanes share every iteration's node load and slab test; only the leaf
 // work (instance entry, triangle test) diverges.  Cornell 1080p: direct 0.185 -> 0.168 ms,
 // indirect 0.311 -> 0.286 ms; scene 1080p emissive 0.476 -> 0.421 ms.
+#if HK_TRAVERSE_PAIRSTEP
+// Two visits per iteration where the order allows it: an inner child-box node p that passes is
+// always followed by node p + 1 (its subtree start, bvh flatten), tested with the same hit
+// distance, so one iteration tests p and — when p is inner and passes — p + 1 too, from one
+// 64-byte load of the two consecutive nodes.  At most one of them is a leaf, whose work (triangle
+// test / instance entry) then follows.  Same visits, tests and results as one node per iteration.
+HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float early_distance, uint32_t exclude)
+{
+    Hit hit;
+    hit.uv = mk2(0.0f, 0.0f);
+    hit.distance = max_distance;
+    hit.instance_index = HK_U32_MAX;
+    hit.primitive_index = HK_U32_MAX;
+    uint32_t top = 0u;                  // next TLAS node
+    uint32_t bot = 0u, bot_count = 0u;  // BLAS walk state (in_bottom: inside an instance)
+    uint32_t bot_base = 0u, prim_offset = 0u, cur_instance = 0u;
+    bool in_bottom = false, intersected = false;
+    Ray local = ray;
+    for (;;) {
+        if (!in_bottom && top >= sc.n_instance_nodes) break;
+        const hk_node* nodes = in_bottom ? sc.asset_nodes + bot_base : sc.instance_nodes;
+        const uint32_t count = in_bottom ? bot_count : sc.n_instance_nodes;
+        const uint32_t index = in_bottom ? bot : top;
+        const uint32_t index2 = index + 1u < count ? index + 1u : index;  // in range; used only when it is p + 1
+        f3 mn, mx, mn2, mx2;
+        uint32_t entry, exit, entry2, exit2;
+        load_node(nodes, index, mn, entry, mx, exit);
+        load_node(nodes, index2, mn2, entry2, mx2, exit2);
+        Ray tr;
+        tr.origin = in_bottom ? local.origin : ray.origin;
+        tr.inv_direction = in_bottom ? local.inv_direction : ray.inv_direction;
+        // BLAS leaves carry their triangle's box (k_fill_blas_leaves, light.wgsl:411-413), TLAS
+        // leaves their instance's min/max (k_fill_tlas_leaves, light.wgsl:456-457)
+        const bool pass = intersects_aabb(tr, mn, mx) < hit.distance;
+        const bool pass2 = intersects_aabb(tr, mn2, mx2) < hit.distance;
+        // the leaf this iteration reaches (if any) and the node after it
+        bool leaf_pass = false;
+        uint32_t leaf_entry = entry, next;
+        if (entry < HK_BVH_LEAF_FLAG) {
+            if (pass) {  // visit p + 1 now
+                if (entry2 < HK_BVH_LEAF_FLAG) {
+                    next = pass2 ? entry2 : exit2;
+                } else {
+                    leaf_pass = pass2;
+                    leaf_entry = entry2;
+                    next = exit2;
+                }
+            } else {
+                next = exit;
+            }
+        } else {
+            leaf_pass = pass;
+            next = exit;
+        }
+        if (in_bottom) {
+            bool stop = false;
+            if (leaf_pass) {
+                const uint32_t primitive_index = prim_offset + leaf_entry - HK_BVH_LEAF_FLAG;
+                f3 a, b, c;
+                load_triangle(sc.primitives, primitive_index, a, b, c);
+                f2 uv;
+                const float d = intersects_triangle(local, a, b, c, uv);
+                if (d < hit.distance) {
+                    hit.distance = d;
+                    hit.uv = uv;
+                    hit.primitive_index = primitive_index;
+                    intersected = true;
+                    stop = d < early_distance;  // traverse_bottom's early return
+                }
+            }
+            bot = next;
+            if (stop || bot >= bot_count) {  // back in traverse_top after traverse_bottom
+                in_bottom = false;
+                if (intersected) {
+                    hit.instance_index = cur_instance;
+                    if (hit.distance < early_distance) return hit;
+                }
+            }
+        } else {
+            top = next;
+            const uint32_t instance_index = leaf_entry - HK_BVH_LEAF_FLAG;
+            if (leaf_pass && instance_index != exclude) {
+                const hk_instance& in = sc.instances[instance_index];
+                local.origin = world_to_local_point(in, ray.origin);
+                local.direction = world_to_local_dir(in, ray.direction);
+                local.inv_direction = inv(local.direction);
+                bot = 0u;
+                bot_count = in.mesh.node[1];
+                bot_base = in.mesh.node[0];
+                prim_offset = in.mesh.primitive;
+                cur_instance = instance_index;
+                intersected = false;
+                in_bottom = bot_count > 0u;  // traverse_bottom over an empty range does nothing
+            }
+        }
+    }
+    return hit;
+}
+#else
 HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float early_distance, uint32_t exclude)
 {
     Hit hit;
@@ -795,6 +946,7 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
     }
     return hit;
 }
+#endif
 
 // ------------------------------------------------------------------ G-buffer visibility
 // Ordered closest-hit traversal, the build's own primary-visibility rule (the reference
