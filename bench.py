@@ -138,6 +138,19 @@ def load_pmc_traffic(config: str, kernel: str):
         return None
 
 
+def load_traversal_bytes(config: str):
+    """Traversal bytes per frame of `config` (nodes, triangles, instances, hit_info of the
+    light passes, priced in reference record sizes) from the committed profiles/traversal_bytes.json
+    (written offline by tools/traversal_bytes.py), if present.  Cache traffic, not HBM bytes."""
+    p = ROOT / "profiles" / "traversal_bytes.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text())["configs"][config]["traversal_bytes_per_frame"]
+    except (KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -335,6 +348,12 @@ def main():
                          "frame_frac": round(frame_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
         }
+        tb = load_traversal_bytes(args.config) if world == 1 and spp == 1 else None
+        if tb is not None:
+            # §8d's second component: node / triangle / instance / hit_info bytes of the light passes
+            # (L1/L2/MALL traffic: the scene is cache resident), over the frame time
+            result["roofline"]["frame_traversal_bytes"] = tb
+            result["roofline"]["frame_traversal_achieved"] = round(tb / (ms * 1e-3) / 1e9, 1)
         if world == 1 and args.cpu_budget > 0:
             result["cpu_baseline"] = cpu_baseline(desc, cam, lights, st, W, H, args.cpu_budget)
         else:

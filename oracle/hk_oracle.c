@@ -470,6 +470,7 @@ unsigned long long hko_stats[4][5];
 static __thread int hko_class = 3;
 static __thread unsigned hko_ray_steps; /* node visits + leaf tests of the current traverse_top */
 uint32_t* hko_steps_out;                 /* per-ray steps of hko_trace, if set */
+unsigned long long hko_hit_infos;        /* hit_info calls (3 vertices + instance + material fetched) */
 #define HKO_STAT(k) (__atomic_fetch_add(&hko_stats[hko_class][k], 1ull, __ATOMIC_RELAXED), hko_ray_steps++)
 #else
 #define HKO_STAT(k) ((void)0)
@@ -568,6 +569,9 @@ static HitInfo empty_hit_info(v3 position, v3 direction)
 static HitInfo hit_info(const hko_ctx* c, const Ray* ray, const Hit* hit)
 {
     HitInfo info;
+#ifdef HKO_STATS
+    __atomic_fetch_add(&hko_hit_infos, 1ull, __ATOMIC_RELAXED);
+#endif
     memset(&info, 0, sizeof(info));
     info.instance_index = hit->instance_index;
     info.material_index = HK_U32_MAX;
