@@ -640,6 +640,50 @@ HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& 
 #ifndef HK_TRAVERSE_PAIRSTEP
 #define HK_TRAVERSE_PAIRSTEP 1
 #endif
+#ifndef HK_WALK_STEPS
+#define HK_WALK_STEPS 2
+#endif
+
+// One iteration of the skip-pointer walk covering up to STEPS consecutive visits: node p and,
+// while the visited node is an inner node whose box passes, its subtree start (the next node of
+// the flattened array, bvh flatten).  All STEPS nodes are loaded and tested up front with the
+// same hit distance (no leaf work happens between such visits).  Returns the node the walk visits
+// next; `leaf_pass`/`leaf_entry` report the leaf reached in this iteration, if its box passed.
+template <int STEPS>
+HKD uint32_t walk_step(const hk_node* nodes, uint32_t index, uint32_t count, const Ray& tr, float distance,
+                       bool& leaf_pass, uint32_t& leaf_entry)
+{
+    uint32_t entry[STEPS], exit[STEPS];
+    bool pass[STEPS];
+#pragma unroll
+    for (int k = 0; k < STEPS; ++k) {
+        const uint32_t i = index + (uint32_t)k < count ? index + (uint32_t)k : index;  // in range; used only when visited
+        f3 mn, mx;
+        load_node(nodes, i, mn, entry[k], mx, exit[k]);
+        pass[k] = intersects_aabb(tr, mn, mx) < distance;
+    }
+    leaf_pass = false;
+    leaf_entry = entry[0];
+    uint32_t next = 0u;
+    bool open = true;  // visits so far were passing inner nodes
+#pragma unroll
+    for (int k = 0; k < STEPS; ++k) {
+        if (open) {
+            if (entry[k] >= HK_BVH_LEAF_FLAG) {
+                leaf_pass = pass[k];
+                leaf_entry = entry[k];
+                next = exit[k];
+                open = false;
+            } else if (!pass[k]) {
+                next = exit[k];
+                open = false;
+            } else {
+                next = entry[k];  // == index + k + 1, visited in this iteration if k + 1 < STEPS
+            }
+        }
+    }
+    return next;
+}
 
 // light.wgsl:400-440 — stackless skip-pointer BLAS walk (reference visit order).
 HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t node_offset, uint32_t node_count,
@@ -648,35 +692,12 @@ HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t nod
     bool intersected = false;
     uint32_t index = 0u;
 #if HK_TRAVERSE_PAIRSTEP
-    // two visits per iteration as in traverse_top below: a passing inner node p is followed by
-    // p + 1 (its subtree start), tested with the same hit distance in the same iteration
+    // up to HK_WALK_STEPS visits per iteration (walk_step), as in traverse_top below
     const hk_node* nodes = sc.asset_nodes + node_offset;
     while (index < node_count) {
-        f3 mn, mx, mn2, mx2;
-        uint32_t entry, exit, entry2, exit2;
-        const uint32_t index2 = index + 1u < node_count ? index + 1u : index;
-        load_node(nodes, index, mn, entry, mx, exit);
-        load_node(nodes, index2, mn2, entry2, mx2, exit2);
-        const bool pass = intersects_aabb(ray, mn, mx) < hit.distance;
-        const bool pass2 = intersects_aabb(ray, mn2, mx2) < hit.distance;
-        bool leaf_pass = false;
-        uint32_t leaf_entry = entry, next;
-        if (entry < HK_BVH_LEAF_FLAG) {
-            if (pass) {
-                if (entry2 < HK_BVH_LEAF_FLAG) {
-                    next = pass2 ? entry2 : exit2;
-                } else {
-                    leaf_pass = pass2;
-                    leaf_entry = entry2;
-                    next = exit2;
-                }
-            } else {
-                next = exit;
-            }
-        } else {
-            leaf_pass = pass;
-            next = exit;
-        }
+        bool leaf_pass;
+        uint32_t leaf_entry;
+        const uint32_t next = walk_step<HK_WALK_STEPS>(nodes, index, node_count, ray, hit.distance, leaf_pass, leaf_entry);
         if (leaf_pass) {
             uint32_t primitive_index = prim_offset + leaf_entry - HK_BVH_LEAF_FLAG;
             f3 a, b, c;
@@ -769,11 +790,12 @@ HKD f3 local_to_world_normal(const hk_instance& in, f3 n)
 // work (instance entry, triangle test) diverges.  Cornell 1080p: direct 0.185 -> 0.168 ms,
 // indirect 0.311 -> 0.286 ms; scene 1080p emissive 0.476 -> 0.421 ms.
 #if HK_TRAVERSE_PAIRSTEP
-// Two visits per iteration where the order allows it: an inner child-box node p that passes is
-// always followed by node p + 1 (its subtree start, bvh flatten), tested with the same hit
-// distance, so one iteration tests p and — when p is inner and passes — p + 1 too, from one
-// 64-byte load of the two consecutive nodes.  At most one of them is a leaf, whose work (triangle
-// test / instance entry) then follows.  Same visits, tests and results as one node per iteration.
+// Several visits per iteration where the order allows it (walk_step): an inner child-box node p
+// that passes is always followed by node p + 1 (its subtree start, bvh flatten), tested with the
+// same hit distance, so one iteration tests p and — while the visited nodes are passing inner
+// nodes — p + 1, p + 2, ... too, from consecutive node loads.  At most one of them is a leaf,
+// whose work (triangle test / instance entry) then follows.  Same visits, tests and results as
+// one node per iteration (HK_WALK_STEPS 2: cornell 1080p 0.619 -> 0.604 ms/frame).
 HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float early_distance, uint32_t exclude)
 {
     Hit hit;
@@ -791,37 +813,15 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
         const hk_node* nodes = in_bottom ? sc.asset_nodes + bot_base : sc.instance_nodes;
         const uint32_t count = in_bottom ? bot_count : sc.n_instance_nodes;
         const uint32_t index = in_bottom ? bot : top;
-        const uint32_t index2 = index + 1u < count ? index + 1u : index;  // in range; used only when it is p + 1
-        f3 mn, mx, mn2, mx2;
-        uint32_t entry, exit, entry2, exit2;
-        load_node(nodes, index, mn, entry, mx, exit);
-        load_node(nodes, index2, mn2, entry2, mx2, exit2);
         Ray tr;
         tr.origin = in_bottom ? local.origin : ray.origin;
         tr.inv_direction = in_bottom ? local.inv_direction : ray.inv_direction;
         // BLAS leaves carry their triangle's box (k_fill_blas_leaves, light.wgsl:411-413), TLAS
-        // leaves their instance's min/max (k_fill_tlas_leaves, light.wgsl:456-457)
-        const bool pass = intersects_aabb(tr, mn, mx) < hit.distance;
-        const bool pass2 = intersects_aabb(tr, mn2, mx2) < hit.distance;
-        // the leaf this iteration reaches (if any) and the node after it
-        bool leaf_pass = false;
-        uint32_t leaf_entry = entry, next;
-        if (entry < HK_BVH_LEAF_FLAG) {
-            if (pass) {  // visit p + 1 now
-                if (entry2 < HK_BVH_LEAF_FLAG) {
-                    next = pass2 ? entry2 : exit2;
-                } else {
-                    leaf_pass = pass2;
-                    leaf_entry = entry2;
-                    next = exit2;
-                }
-            } else {
-                next = exit;
-            }
-        } else {
-            leaf_pass = pass;
-            next = exit;
-        }
+        // leaves their instance's min/max (k_fill_tlas_leaves, light.wgsl:456-457); the leaf this
+        // iteration reaches (if any) and the node after it
+        bool leaf_pass;
+        uint32_t leaf_entry;
+        const uint32_t next = walk_step<HK_WALK_STEPS>(nodes, index, count, tr, hit.distance, leaf_pass, leaf_entry);
         if (in_bottom) {
             bool stop = false;
             if (leaf_pass) {
