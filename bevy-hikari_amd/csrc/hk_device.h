@@ -643,6 +643,9 @@ HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& 
 #ifndef HK_WALK_STEPS
 #define HK_WALK_STEPS 2
 #endif
+#ifndef HK_WALK_EAGER
+#define HK_WALK_EAGER 0
+#endif
 
 // One iteration of the skip-pointer walk covering up to STEPS consecutive visits: node p and,
 // while the visited node is an inner node whose box passes, its subtree start (the next node of
@@ -654,14 +657,21 @@ HKD uint32_t walk_step(const hk_node* nodes, uint32_t index, uint32_t count, con
                        bool& leaf_pass, uint32_t& leaf_entry)
 {
     uint32_t entry[STEPS], exit[STEPS];
+    f3 mn[STEPS], mx[STEPS];
     bool pass[STEPS];
 #pragma unroll
     for (int k = 0; k < STEPS; ++k) {
         const uint32_t i = index + (uint32_t)k < count ? index + (uint32_t)k : index;  // in range; used only when visited
-        f3 mn, mx;
-        load_node(nodes, i, mn, entry[k], mx, exit[k]);
-        pass[k] = intersects_aabb(tr, mn, mx) < distance;
+        load_node(nodes, i, mn[k], entry[k], mx[k], exit[k]);
     }
+#if HK_WALK_EAGER
+    // all STEPS node loads issued together (the compiler otherwise sinks node p + 1's load into
+    // the branch that uses it, after node p's test: two dependent load latencies per iteration)
+#pragma unroll
+    for (int k = 0; k < STEPS; ++k) __asm__ volatile("" ::"v"(mn[k].x), "v"(mx[k].x));
+#endif
+#pragma unroll
+    for (int k = 0; k < STEPS; ++k) pass[k] = intersects_aabb(tr, mn[k], mx[k]) < distance;
     leaf_pass = false;
     leaf_entry = entry[0];
     uint32_t next = 0u;
