@@ -76,6 +76,21 @@ struct hk_ctx {
     float4* g_velocity_uv = nullptr;
     float4* g_prev_position = nullptr;    // the previous frame's planes (prepass.rs:309-317 swap)
     float4* g_prev_velocity_uv = nullptr;
+    // the other slot of the planes k_gbuffer double-buffers (swapped with the current ones on each
+    // hk_render_gbuffer, like position / velocity above) so a frame's G-buffer can be traced ahead
+    uint32_t* g_prev_normal = nullptr;
+    float2* g_prev_depth_gradient = nullptr;
+    float2* g_prev_instance_material = nullptr;
+    uint2* albedo_prev = nullptr;
+    // G-buffer pipelining: k_gbuffer of frame f runs on gb_stream, next to frame f-1's light passes
+    hipStream_t gb_stream = nullptr;
+    hipEvent_t ev_gb_done = nullptr;            // after the latest k_gbuffer launch (either stream)
+    hipEvent_t ev_gb_call[2] = {nullptr, nullptr};  // caller stream at the entry of the last two calls
+    hipEvent_t ev_post = nullptr;               // after a post-process read of the previous slot
+    bool gb_pending = false;                    // a k_gbuffer launch was made on gb_stream
+    bool gb_serial = true;                      // the next k_gbuffer runs in caller-stream order
+    bool post_pending = false;
+    uint32_t gb_calls = 0;
     uint32_t head = 0;                    // frame_number % 2 (PostProcessTextures.head)
     // channel fork-join: emissive and indirect passes on side streams next to direct_lit
     hipStream_t side[2] = {nullptr, nullptr};
@@ -128,6 +143,30 @@ int fail(hk_ctx* c, int code, const std::string& msg)
 
 hipStream_t pick(hk_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
 
+#define HK_TRY(expr)            \
+    do {                        \
+        int _r = (expr);        \
+        if (_r != HK_OK) return _r; \
+    } while (0)
+
+// Work that reads G-buffer planes, counters or targets, or that changes the scene, first waits
+// for any k_gbuffer launched ahead on gb_stream (hipStreamWaitEvent: device-side, no host wait).
+int gb_join(hk_ctx* c, hipStream_t st)
+{
+    if (c->gb_pending && hipStreamWaitEvent(st, c->ev_gb_done, 0) != hipSuccess)
+        return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(G-buffer) failed");
+    return HK_OK;
+}
+// the scene, sizes or G-buffer planes change on the caller's stream: the next k_gbuffer must run
+// in caller-stream order (and a synchronous change waits for the one in flight)
+int gb_serialize(hk_ctx* c, bool host_sync)
+{
+    c->gb_serial = true;
+    if (host_sync && c->gb_stream && hipStreamSynchronize(c->gb_stream) != hipSuccess)
+        return fail(c, HK_ERR_HIP, "hipStreamSynchronize(G-buffer stream) failed");
+    return HK_OK;
+}
+
 template <typename T>
 void release(T*& p)
 {
@@ -161,6 +200,12 @@ void free_targets(hk_ctx* c)
     release(c->upscale);
     release(c->g_prev_position);
     release(c->g_prev_velocity_uv);
+    release(c->g_prev_normal);
+    release(c->g_prev_depth_gradient);
+    release(c->g_prev_instance_material);
+    release(c->albedo_prev);
+    c->gb_serial = true;
+    c->gb_calls = 0;
     c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
     release(c->accum);
     release(c->accum_out);
@@ -387,7 +432,12 @@ int hk_create(int device, hk_ctx** out)
             hk_destroy(c);
             return HK_ERR_HIP;
         }
-    if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gb_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gb_call[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gb_call[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess) {
         hk_destroy(c);
         return HK_ERR_HIP;
     }
@@ -399,6 +449,7 @@ void hk_destroy(hk_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->gb_stream) (void)hipStreamSynchronize(c->gb_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_targets(c);
     for (int i = 0; i < 9; ++i) release(c->buf[i]);
@@ -424,6 +475,9 @@ void hk_destroy(hk_ctx* c)
         if (c->ev_join[k]) (void)hipEventDestroy(c->ev_join[k]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    for (hipEvent_t e : {c->ev_gb_done, c->ev_gb_call[0], c->ev_gb_call[1], c->ev_post})
+        if (e) (void)hipEventDestroy(e);
+    if (c->gb_stream) (void)hipStreamDestroy(c->gb_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -434,6 +488,7 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
 {
     if (!c || !d) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
+    HK_TRY(gb_serialize(c, true));
     const hk_array* arr[9] = {&d->vertices, &d->primitives, &d->asset_nodes, &d->alias_table, &d->instances,
                               &d->instance_nodes, &d->materials, &d->emissive_nodes, &d->emissives};
     const size_t elem[9] = {sizeof(hk_vertex), sizeof(hk_primitive), sizeof(hk_node), sizeof(hk_alias_entry),
@@ -542,6 +597,8 @@ int hk_update_instances(hk_ctx* c, const float* models, const float* local_aabbs
         return fail(c, HK_ERR_STATE, "scene BVHs are not bvh-0.7.1 flattened (3n - 2 nodes); cannot rebuild");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
+    HK_TRY(gb_serialize(c, false));
     const uint32_t n = count, m = c->count[8], n_alias = c->count[3];
     const uint32_t nm = n > m ? n : m;
     auto align = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -623,6 +680,7 @@ int hk_texture_upload(hk_ctx* c, const hk_texture* t, uint32_t count)
 {
     if (!c || (count && !t)) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
+    HK_TRY(gb_serialize(c, true));
     std::vector<hk_texture_desc> desc(count);
     uint64_t total = 0;
     for (uint32_t i = 0; i < count; ++i) {
@@ -661,6 +719,7 @@ int hk_set_noise(hk_ctx* c, const uint8_t* rgba, uint32_t count, uint32_t size)
     if (!c || !rgba) return HK_ERR_INVALID;
     if (count != 16 || size != 64) return fail(c, HK_ERR_INVALID, "blue noise must be 16 textures of 64x64 RGBA8");
     (void)hipSetDevice(c->device);
+    HK_TRY(gb_serialize(c, true));
     if (!c->noise) HK_HIP(c, hipMalloc(&c->noise, 16 * 64 * 64 * 4));
     HK_HIP(c, hipMemcpy(c->noise, rgba, 16 * 64 * 64 * 4, hipMemcpyHostToDevice));
     c->has_noise = true;
@@ -704,6 +763,7 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
         whole = false;
     }
     HK_HIP(c, hipStreamSynchronize(c->stream));
+    HK_HIP(c, hipStreamSynchronize(c->gb_stream));
     free_targets(c);
     c->albedo_fresh = false;
     c->S[0] = width;
@@ -746,6 +806,14 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     HK_HIP(c, hipMalloc(&c->g_prev_velocity_uv, SP * sizeof(float4)));
     HK_HIP(c, hipMemset(c->g_prev_position, 0, SP * sizeof(float4)));
     HK_HIP(c, hipMemset(c->g_prev_velocity_uv, 0, SP * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->g_prev_normal, SP * sizeof(uint32_t)));
+    HK_HIP(c, hipMalloc(&c->g_prev_depth_gradient, SP * sizeof(float2)));
+    HK_HIP(c, hipMalloc(&c->g_prev_instance_material, SP * sizeof(float2)));
+    HK_HIP(c, hipMalloc(&c->albedo_prev, SP * sizeof(uint2)));
+    HK_HIP(c, hipMemset(c->g_prev_normal, 0, SP * sizeof(uint32_t)));
+    HK_HIP(c, hipMemset(c->g_prev_depth_gradient, 0, SP * sizeof(float2)));
+    HK_HIP(c, hipMemset(c->g_prev_instance_material, 0, SP * sizeof(float2)));
+    HK_HIP(c, hipMemset(c->albedo_prev, 0, SP * sizeof(uint2)));
     HK_HIP(c, hipMalloc(&c->albedo, SP * sizeof(uint2)));
     HK_HIP(c, hipMemset(c->g_position, 0, SP * sizeof(float4)));
     HK_HIP(c, hipMemset(c->g_normal, 0, SP * sizeof(uint32_t)));
@@ -811,9 +879,31 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         return fail(c, HK_ERR_INVALID, "scene BVH too deep for the G-buffer traversal stack (TLAS + BLAS depth > 64)");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    // Pipelining: this frame's planes go to the slot frame f-2 used.  Its readers are the work
+    // enqueued on the caller's stream before the previous hk_render_gbuffer call (frame f-2's
+    // passes, denoise, tone-sum, readbacks) and a post-process of frame f-1 (it reads the previous
+    // slot); k_gbuffer waits for exactly those on gb_stream and so overlaps frame f-1's light
+    // passes.  A scene / size / plane change since the last call serialises it instead.
+    static const bool pipeline = !getenv("HK_GB_PIPELINE") || getenv("HK_GB_PIPELINE")[0] != '0';
+    const uint32_t e = c->gb_calls & 1u;
+    HK_HIP(c, hipEventRecord(c->ev_gb_call[e], st));
+    hipStream_t gs = st;
+    if (pipeline && !c->gb_serial && c->gb_calls > 0) {
+        gs = c->gb_stream;
+        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[e ^ 1u], 0));
+        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_done, 0));  // the previous k_gbuffer (if it ran on st)
+        if (c->post_pending) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_post, 0));
+    } else {
+        HK_TRY(gb_join(c, st));
+    }
+    c->post_pending = false;
     // a new frame: this frame's planes replace the previous ones (prepass.rs:309-317)
     std::swap(c->g_position, c->g_prev_position);
     std::swap(c->g_velocity_uv, c->g_prev_velocity_uv);
+    std::swap(c->g_normal, c->g_prev_normal);
+    std::swap(c->g_depth_gradient, c->g_prev_depth_gradient);
+    std::swap(c->g_instance_material, c->g_prev_instance_material);
+    std::swap(c->albedo, c->albedo_prev);
     c->head = in->frame_number & 1u;
     FrameArgs A = frame_args(c, nullptr, in);
     ViewArgs V;
@@ -822,7 +912,11 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     std::memcpy(V.inverse_view_proj, in->view.inverse_view_proj, sizeof(V.inverse_view_proj));
     // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
     // hk_render_frame runs it on its own only for host-supplied G-buffers
-    timed(c, "gbuffer", st, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, st); });
+    timed(c, "gbuffer", gs, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, gs); });
+    HK_HIP(c, hipEventRecord(c->ev_gb_done, gs));
+    if (gs != st) c->gb_pending = true;
+    c->gb_serial = false;
+    c->gb_calls++;
     c->albedo_fresh = true;
     HK_HIP(c, hipGetLastError());
     return HK_OK;
@@ -855,6 +949,8 @@ int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, i
     }
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
+    c->gb_serial = true;
     HK_HIP(c, hipMemcpyAsync(dst, data, bytes, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
     if (!device_ptr) HK_HIP(c, hipStreamSynchronize(st));
     return HK_OK;
@@ -884,6 +980,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
         return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     c->head = in->frame_number & 1u;
@@ -939,6 +1036,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     if (c->stripe_n >= 2) return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude the denoiser: it reads neighbours");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     FrameArgs A = frame_args(c, settings, in);
     int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
     DenoiseArgs D;
@@ -967,6 +1065,7 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     if (!settings) return fail(c, HK_ERR_INVALID, "null settings");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     hk_frame_inputs dummy;
     std::memset(&dummy, 0, sizeof(dummy));
     FrameArgs A = frame_args(c, settings, &dummy);
@@ -988,6 +1087,7 @@ int hk_post_process(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in,
     if (c->S_rows != (int32_t)c->S[1]) return fail(c, HK_ERR_STATE, "hk_post_process needs a whole-frame context");
     (void)hipSetDevice(c->device);
     hipStream_t s = pick(c, stream);
+    HK_TRY(gb_join(c, s));
     c->head = in->frame_number & 1u;
     const uint32_t head = c->head;
     // post_process.rs:663-731 sizes: ceil(S * scale), scale = 1 / ratio, x 2 after SMAA TU4x
@@ -1040,6 +1140,9 @@ int hk_post_process(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in,
         P.in.output = hk_pp_out{(uint16_t*)c->taa_buf[head], T0, T1};
         timed(c, "taa_jasmine", s, [&] { launch_taa(P, s); });
     }
+    // the next k_gbuffer overwrites the previous-frame planes read here
+    HK_HIP(c, hipEventRecord(c->ev_post, s));
+    c->post_pending = true;
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -1050,6 +1153,7 @@ int hk_accumulate(hk_ctx* c, int reset, void* stream)
     if (rc) return rc;
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
     if (!c->accum) {
         HK_HIP(c, hipMalloc(&c->accum, n * sizeof(float4)));
@@ -1071,6 +1175,7 @@ int hk_resolve_accumulation(hk_ctx* c, void* stream)
     if (!c->accum || c->accum_n == 0) return fail(c, HK_ERR_STATE, "nothing accumulated (hk_accumulate)");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
     timed(c, "resolve", st, [&] { launch_resolve(c->accum, (uint32_t)n, (float)c->accum_n, c->accum_out, st); });
     HK_HIP(c, hipGetLastError());
@@ -1130,6 +1235,7 @@ int hk_get_output(hk_ctx* c, int id, void* dst, size_t bytes, int to_host, void*
     if (bytes != need) return fail(c, HK_ERR_INVALID, "output size mismatch");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     HK_HIP(c, hipMemcpyAsync(dst, p, bytes, to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
     if (to_host) HK_HIP(c, hipStreamSynchronize(st));
     return HK_OK;
@@ -1145,6 +1251,7 @@ int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* d
     if (row0 + rows > h) return fail(c, HK_ERR_INVALID, "row range outside the plane");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     size_t pitch = (size_t)w * b;
     HK_HIP(c, hipMemcpyAsync(dst, (const char*)p + (size_t)row0 * pitch, (size_t)rows * pitch,
                              to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
@@ -1159,6 +1266,7 @@ int hk_dump_reservoirs(hk_ctx* c, int id, hk_packed_reservoir* dst, size_t count
     if (count != c->res_n) return fail(c, HK_ERR_INVALID, "reservoir count mismatch");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     std::vector<uint4> planes((size_t)4 * c->res_n);
     HK_HIP(c, hipMemcpyAsync(planes.data(), c->reservoirs[id], planes.size() * sizeof(uint4), hipMemcpyDeviceToHost, st));
     HK_HIP(c, hipStreamSynchronize(st));
@@ -1176,6 +1284,7 @@ int hk_load_reservoirs(hk_ctx* c, int id, const hk_packed_reservoir* src, size_t
     if (count != c->res_n) return fail(c, HK_ERR_INVALID, "reservoir count mismatch");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     std::vector<uint4> planes((size_t)4 * c->res_n);
     for (size_t i = 0; i < count; ++i) {
         const uint4* s = reinterpret_cast<const uint4*>(src + i);
@@ -1190,6 +1299,7 @@ int hk_reset_counters(hk_ctx* c, void* stream)
 {
     if (!c) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
+    HK_TRY(gb_join(c, pick(c, stream)));
     HK_HIP(c, hipMemsetAsync(c->counters, 0, COUNTER_BYTES, pick(c, stream)));
     return HK_OK;
 }
@@ -1199,6 +1309,7 @@ int hk_read_counters(hk_ctx* c, hk_counters* out, void* stream)
     if (!c || !out) return HK_ERR_INVALID;
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     std::vector<unsigned long long> v(3 * COUNTER_SPAN);
     HK_HIP(c, hipMemcpyAsync(v.data(), c->counters, COUNTER_BYTES, hipMemcpyDeviceToHost, st));
     HK_HIP(c, hipStreamSynchronize(st));
@@ -1242,6 +1353,7 @@ int hk_trace(hk_ctx* c, const float* rays, const float* max_d, const float* earl
     if (n == 0) return HK_OK;
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
     FrameArgs A = frame_args(c, nullptr, nullptr);
     if (device_ptrs) {
         launch_trace(A.sc, rays, max_d, early_d, excl, n, (uint32_t*)hits, c->counters, st);
