@@ -91,6 +91,18 @@ struct hk_ctx {
     bool gb_serial = true;                      // the next k_gbuffer runs in caller-stream order
     bool post_pending = false;
     uint32_t gb_calls = 0;
+    // Denoise pipelining: demodulation, the a-trous levels and the tone-sum of frame f run on
+    // dn_stream next to frame f+1's light passes; render / variance are double-buffered for it
+    uint2* render_alt[3] = {};
+    float* variance_alt[3] = {};
+    hipStream_t dn_stream = nullptr;
+    hipEvent_t ev_rf = nullptr;                 // caller stream, end of the latest hk_render_frame
+    hipEvent_t ev_dn[2] = {nullptr, nullptr};   // dn_stream, end of denoise call k (+ its tone-sum), k & 1
+    hipEvent_t ev_dn_last = nullptr;            // dn_stream, after its latest work
+    uint32_t dn_k = 0;                          // denoise calls queued on dn_stream
+    bool dn_pending = false;                    // work was queued on dn_stream
+    bool rf_swapped = false;                    // the latest hk_render_frame wrote the other render slot
+    bool dn_frame = false;                      // the latest frame's denoise went to dn_stream
     uint32_t head = 0;                    // frame_number % 2 (PostProcessTextures.head)
     // channel fork-join: emissive and indirect passes on side streams next to direct_lit
     hipStream_t side[2] = {nullptr, nullptr};
@@ -150,12 +162,20 @@ hipStream_t pick(hk_ctx* c, void* stream) { return stream ? (hipStream_t)stream 
     } while (0)
 
 // Work that reads G-buffer planes, counters or targets, or that changes the scene, first waits
-// for any k_gbuffer launched ahead on gb_stream (hipStreamWaitEvent: device-side, no host wait).
-int gb_join(hk_ctx* c, hipStream_t st)
+// for any k_gbuffer launched ahead on gb_stream and any denoise / tone-sum queued on dn_stream
+// (hipStreamWaitEvent: device-side, no host wait).
+int gb_join(hk_ctx* c, hipStream_t st, bool with_denoise = true)
 {
     if (c->gb_pending && hipStreamWaitEvent(st, c->ev_gb_done, 0) != hipSuccess)
         return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(G-buffer) failed");
+    if (with_denoise && c->dn_pending && hipStreamWaitEvent(st, c->ev_dn_last, 0) != hipSuccess)
+        return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(denoise) failed");
     return HK_OK;
+}
+bool dn_pipeline_enabled()
+{
+    static const bool on = !getenv("HK_DN_PIPELINE") || getenv("HK_DN_PIPELINE")[0] != '0';
+    return on;
 }
 // the scene, sizes or G-buffer planes change on the caller's stream: the next k_gbuffer must run
 // in caller-stream order (and a synchronous change waits for the one in flight)
@@ -164,6 +184,8 @@ int gb_serialize(hk_ctx* c, bool host_sync)
     c->gb_serial = true;
     if (host_sync && c->gb_stream && hipStreamSynchronize(c->gb_stream) != hipSuccess)
         return fail(c, HK_ERR_HIP, "hipStreamSynchronize(G-buffer stream) failed");
+    if (host_sync && c->dn_stream && hipStreamSynchronize(c->dn_stream) != hipSuccess)
+        return fail(c, HK_ERR_HIP, "hipStreamSynchronize(denoise stream) failed");
     return HK_OK;
 }
 
@@ -185,6 +207,8 @@ void free_targets(hk_ctx* c)
     for (int i = 0; i < 3; ++i) {
         release(c->variance[i]);
         release(c->render[i]);
+        release(c->variance_alt[i]);
+        release(c->render_alt[i]);
         release(c->denoised[i]);
     }
     for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) release(c->reservoirs[i]);
@@ -206,6 +230,8 @@ void free_targets(hk_ctx* c)
     release(c->albedo_prev);
     c->gb_serial = true;
     c->gb_calls = 0;
+    c->dn_k = 0;
+    c->rf_swapped = c->dn_frame = false;
     c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
     release(c->accum);
     release(c->accum_out);
@@ -437,7 +463,12 @@ int hk_create(int device, hk_ctx** out)
         hipEventCreateWithFlags(&c->ev_gb_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rf, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_dn[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_dn[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_dn_last, hipEventDisableTiming) != hipSuccess) {
         hk_destroy(c);
         return HK_ERR_HIP;
     }
@@ -450,6 +481,7 @@ void hk_destroy(hk_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->gb_stream) (void)hipStreamSynchronize(c->gb_stream);
+    if (c->dn_stream) (void)hipStreamSynchronize(c->dn_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_targets(c);
     for (int i = 0; i < 9; ++i) release(c->buf[i]);
@@ -475,9 +507,11 @@ void hk_destroy(hk_ctx* c)
         if (c->ev_join[k]) (void)hipEventDestroy(c->ev_join[k]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    for (hipEvent_t e : {c->ev_gb_done, c->ev_gb_call[0], c->ev_gb_call[1], c->ev_post})
+    for (hipEvent_t e : {c->ev_gb_done, c->ev_gb_call[0], c->ev_gb_call[1], c->ev_post, c->ev_rf, c->ev_dn[0],
+                         c->ev_dn[1], c->ev_dn_last})
         if (e) (void)hipEventDestroy(e);
     if (c->gb_stream) (void)hipStreamDestroy(c->gb_stream);
+    if (c->dn_stream) (void)hipStreamDestroy(c->dn_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -764,6 +798,7 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     }
     HK_HIP(c, hipStreamSynchronize(c->stream));
     HK_HIP(c, hipStreamSynchronize(c->gb_stream));
+    HK_HIP(c, hipStreamSynchronize(c->dn_stream));
     free_targets(c);
     c->albedo_fresh = false;
     c->S[0] = width;
@@ -827,6 +862,10 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
         HK_HIP(c, hipMalloc(&c->denoised[i], sp * sizeof(uint2)));
         HK_HIP(c, hipMemset(c->variance[i], 0, sp * sizeof(float)));
         HK_HIP(c, hipMemset(c->render[i], 0, sp * sizeof(uint2)));
+        HK_HIP(c, hipMalloc(&c->variance_alt[i], sp * sizeof(float)));
+        HK_HIP(c, hipMalloc(&c->render_alt[i], sp * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->variance_alt[i], 0, sp * sizeof(float)));
+        HK_HIP(c, hipMemset(c->render_alt[i], 0, sp * sizeof(uint2)));
         HK_HIP(c, hipMemset(c->denoised[i], 0, sp * sizeof(uint2)));
     }
     c->res_n = (uint32_t)sp;
@@ -893,6 +932,8 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[e ^ 1u], 0));
         HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_done, 0));  // the previous k_gbuffer (if it ran on st)
         if (c->post_pending) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_post, 0));
+        // frame f-2's denoise on dn_stream read that slot (the latest denoise call is frame f-1's)
+        if (c->dn_k >= 2) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_dn[c->dn_k & 1u], 0));
     } else {
         HK_TRY(gb_join(c, st));
     }
@@ -980,7 +1021,20 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
-    HK_TRY(gb_join(c, st));
+    // Denoise pipelining: with the denoiser on and all three channels rendered, this frame's
+    // render / variance targets are the other slot, last read by frame f-2's denoise and tone-sum
+    // (the latest denoise call is frame f-1's), so frame f-1's denoise can still be running.
+    const bool swap = dn_pipeline_enabled() && settings->denoise && settings->indirect_bounces >= 1u && c->stripe_n < 2;
+    HK_TRY(gb_join(c, st, !swap));
+    if (swap) {
+        for (int ch = 0; ch < 3; ++ch) {
+            std::swap(c->render[ch], c->render_alt[ch]);
+            std::swap(c->variance[ch], c->variance_alt[ch]);
+        }
+        if (c->dn_k >= 2) HK_HIP(c, hipStreamWaitEvent(st, c->ev_dn[c->dn_k & 1u], 0));
+    }
+    c->rf_swapped = swap;
+    c->dn_frame = false;
     if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
         return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     c->head = in->frame_number & 1u;
@@ -1023,6 +1077,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         HK_HIP(c, hipEventRecord(c->ev_join[1], s2));
         HK_HIP(c, hipStreamWaitEvent(st, c->ev_join[1], 0));
     }
+    if (swap) HK_HIP(c, hipEventRecord(c->ev_rf, st));
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -1035,8 +1090,12 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     if (!settings->denoise) return HK_OK;
     if (c->stripe_n >= 2) return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude the denoiser: it reads neighbours");
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
-    HK_TRY(gb_join(c, st));
+    hipStream_t caller = pick(c, stream);
+    // after a slot-swapping hk_render_frame: on dn_stream, next to the following frame's passes
+    const bool async = c->rf_swapped;
+    hipStream_t st = async ? c->dn_stream : caller;
+    if (async) HK_HIP(c, hipStreamWaitEvent(st, c->ev_rf, 0));
+    else HK_TRY(gb_join(c, st));
     FrameArgs A = frame_args(c, settings, in);
     int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
     DenoiseArgs D;
@@ -1054,6 +1113,14 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     c->last_denoised_channels = channels;
     timed(c, "demodulation", st, [&] { launch_demod(A, D, st); });
     for (int level = 0; level < 4; ++level) timed(c, "denoise", st, [&] { launch_denoise(A, D, level, st); });
+    if (async) {
+        HK_HIP(c, hipEventRecord(c->ev_dn[c->dn_k & 1u], st));
+        HK_HIP(c, hipEventRecord(c->ev_dn_last, st));
+        c->dn_k++;
+        c->dn_pending = true;
+    }
+    c->rf_swapped = false;
+    c->dn_frame = async;
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -1064,8 +1131,10 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     if (rc) return rc;
     if (!settings) return fail(c, HK_ERR_INVALID, "null settings");
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
-    HK_TRY(gb_join(c, st));
+    // after a denoise queued on dn_stream, the tone-sum of that frame follows it there
+    const bool async = c->dn_frame && settings->denoise;
+    hipStream_t st = async ? c->dn_stream : pick(c, stream);
+    if (!async) HK_TRY(gb_join(c, st));
     hk_frame_inputs dummy;
     std::memset(&dummy, 0, sizeof(dummy));
     FrameArgs A = frame_args(c, settings, &dummy);
@@ -1075,6 +1144,11 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     T.indirect = settings->indirect_bounces == 0u ? nullptr : (settings->denoise ? c->denoised[2] : c->render[2]);
     T.output = c->tone_buf[c->head];
     timed(c, "tone_mapping", st, [&] { launch_tone(A, T, st); });
+    if (async) {
+        HK_HIP(c, hipEventRecord(c->ev_dn[(c->dn_k - 1u) & 1u], st));
+        HK_HIP(c, hipEventRecord(c->ev_dn_last, st));
+    }
+    c->dn_frame = false;
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
