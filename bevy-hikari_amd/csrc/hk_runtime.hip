@@ -91,18 +91,21 @@ struct hk_ctx {
     bool gb_serial = true;                      // the next k_gbuffer runs in caller-stream order
     bool post_pending = false;
     uint32_t gb_calls = 0;
-    // Denoise pipelining: demodulation, the a-trous levels and the tone-sum of frame f run on
-    // dn_stream next to frame f+1's light passes; render / variance are double-buffered for it
+    // Frame-tail pipelining: the demodulation, a-trous levels and tone-sum of frame f run on
+    // dn_stream next to frame f+1's light passes; render / variance are double-buffered for it.
+    // Slot events: the latest tail work that read render slot r / G-buffer slot g.
     uint2* render_alt[3] = {};
     float* variance_alt[3] = {};
     hipStream_t dn_stream = nullptr;
     hipEvent_t ev_rf = nullptr;                 // caller stream, end of the latest hk_render_frame
-    hipEvent_t ev_dn[2] = {nullptr, nullptr};   // dn_stream, end of denoise call k (+ its tone-sum), k & 1
+    hipEvent_t ev_rslot[2] = {nullptr, nullptr};
+    hipEvent_t ev_gslot[2] = {nullptr, nullptr};
     hipEvent_t ev_dn_last = nullptr;            // dn_stream, after its latest work
-    uint32_t dn_k = 0;                          // denoise calls queued on dn_stream
+    bool rslot_rec[2] = {false, false}, gslot_rec[2] = {false, false};
+    uint32_t rslot = 0, gslot = 0;              // current render / G-buffer slot
     bool dn_pending = false;                    // work was queued on dn_stream
     bool rf_swapped = false;                    // the latest hk_render_frame wrote the other render slot
-    bool dn_frame = false;                      // the latest frame's denoise went to dn_stream
+    bool tail_open = false;                     // dn_stream already waits for that frame (ev_rf)
     uint32_t head = 0;                    // frame_number % 2 (PostProcessTextures.head)
     // channel fork-join: emissive and indirect passes on side streams next to direct_lit
     hipStream_t side[2] = {nullptr, nullptr};
@@ -172,6 +175,25 @@ int gb_join(hk_ctx* c, hipStream_t st, bool with_denoise = true)
         return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(denoise) failed");
     return HK_OK;
 }
+// frame-tail work on dn_stream: it starts after the frame's hk_render_frame (ev_rf) and marks
+// the render / G-buffer slots it read
+int tail_begin(hk_ctx* c)
+{
+    if (!c->tail_open && hipStreamWaitEvent(c->dn_stream, c->ev_rf, 0) != hipSuccess)
+        return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(frame) failed");
+    c->tail_open = true;
+    return HK_OK;
+}
+int tail_end(hk_ctx* c)
+{
+    if (hipEventRecord(c->ev_rslot[c->rslot], c->dn_stream) != hipSuccess ||
+        hipEventRecord(c->ev_gslot[c->gslot], c->dn_stream) != hipSuccess ||
+        hipEventRecord(c->ev_dn_last, c->dn_stream) != hipSuccess)
+        return fail(c, HK_ERR_HIP, "hipEventRecord(frame tail) failed");
+    c->rslot_rec[c->rslot] = c->gslot_rec[c->gslot] = true;
+    c->dn_pending = true;
+    return HK_OK;
+}
 bool dn_pipeline_enabled()
 {
     static const bool on = !getenv("HK_DN_PIPELINE") || getenv("HK_DN_PIPELINE")[0] != '0';
@@ -230,8 +252,8 @@ void free_targets(hk_ctx* c)
     release(c->albedo_prev);
     c->gb_serial = true;
     c->gb_calls = 0;
-    c->dn_k = 0;
-    c->rf_swapped = c->dn_frame = false;
+    c->rf_swapped = c->tail_open = false;
+    c->rslot_rec[0] = c->rslot_rec[1] = c->gslot_rec[0] = c->gslot_rec[1] = false;
     c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
     release(c->accum);
     release(c->accum_out);
@@ -466,8 +488,10 @@ int hk_create(int device, hk_ctx** out)
         hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rf, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_dn[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_dn[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rslot[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rslot[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gslot[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gslot[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_dn_last, hipEventDisableTiming) != hipSuccess) {
         hk_destroy(c);
         return HK_ERR_HIP;
@@ -507,8 +531,8 @@ void hk_destroy(hk_ctx* c)
         if (c->ev_join[k]) (void)hipEventDestroy(c->ev_join[k]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    for (hipEvent_t e : {c->ev_gb_done, c->ev_gb_call[0], c->ev_gb_call[1], c->ev_post, c->ev_rf, c->ev_dn[0],
-                         c->ev_dn[1], c->ev_dn_last})
+    for (hipEvent_t e : {c->ev_gb_done, c->ev_gb_call[0], c->ev_gb_call[1], c->ev_post, c->ev_rf, c->ev_rslot[0],
+                         c->ev_rslot[1], c->ev_gslot[0], c->ev_gslot[1], c->ev_dn_last})
         if (e) (void)hipEventDestroy(e);
     if (c->gb_stream) (void)hipStreamDestroy(c->gb_stream);
     if (c->dn_stream) (void)hipStreamDestroy(c->dn_stream);
@@ -932,8 +956,8 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[e ^ 1u], 0));
         HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_done, 0));  // the previous k_gbuffer (if it ran on st)
         if (c->post_pending) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_post, 0));
-        // frame f-2's denoise on dn_stream read that slot (the latest denoise call is frame f-1's)
-        if (c->dn_k >= 2) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_dn[c->dn_k & 1u], 0));
+        // frame f-2's denoise on dn_stream read that slot
+        if (c->gslot_rec[c->gslot ^ 1u]) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gslot[c->gslot ^ 1u], 0));
     } else {
         HK_TRY(gb_join(c, st));
     }
@@ -945,6 +969,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     std::swap(c->g_depth_gradient, c->g_prev_depth_gradient);
     std::swap(c->g_instance_material, c->g_prev_instance_material);
     std::swap(c->albedo, c->albedo_prev);
+    c->gslot ^= 1u;
     c->head = in->frame_number & 1u;
     FrameArgs A = frame_args(c, nullptr, in);
     ViewArgs V;
@@ -1021,20 +1046,22 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
-    // Denoise pipelining: with the denoiser on and all three channels rendered, this frame's
-    // render / variance targets are the other slot, last read by frame f-2's denoise and tone-sum
-    // (the latest denoise call is frame f-1's), so frame f-1's denoise can still be running.
-    const bool swap = dn_pipeline_enabled() && settings->denoise && settings->indirect_bounces >= 1u && c->stripe_n < 2;
-    HK_TRY(gb_join(c, st, !swap));
+    // Frame-tail pipelining: with all three channels rendered, this frame's render / variance
+    // targets are the other slot, last read by frame f-2's denoise / tone-sum, so frame f-1's tail
+    // (on dn_stream) can still be running while this frame's light passes start.
+    const bool swap = dn_pipeline_enabled() && settings->indirect_bounces >= 1u;
+    // (k_albedo rewrites the albedo plane a previous tail may still read: full join then)
+    HK_TRY(gb_join(c, st, !swap || !c->albedo_fresh));
     if (swap) {
         for (int ch = 0; ch < 3; ++ch) {
             std::swap(c->render[ch], c->render_alt[ch]);
             std::swap(c->variance[ch], c->variance_alt[ch]);
         }
-        if (c->dn_k >= 2) HK_HIP(c, hipStreamWaitEvent(st, c->ev_dn[c->dn_k & 1u], 0));
+        c->rslot ^= 1u;
+        if (c->rslot_rec[c->rslot]) HK_HIP(c, hipStreamWaitEvent(st, c->ev_rslot[c->rslot], 0));
     }
     c->rf_swapped = swap;
-    c->dn_frame = false;
+    c->tail_open = false;
     if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
         return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     c->head = in->frame_number & 1u;
@@ -1094,7 +1121,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     // after a slot-swapping hk_render_frame: on dn_stream, next to the following frame's passes
     const bool async = c->rf_swapped;
     hipStream_t st = async ? c->dn_stream : caller;
-    if (async) HK_HIP(c, hipStreamWaitEvent(st, c->ev_rf, 0));
+    if (async) HK_TRY(tail_begin(c));
     else HK_TRY(gb_join(c, st));
     FrameArgs A = frame_args(c, settings, in);
     int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
@@ -1113,14 +1140,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     c->last_denoised_channels = channels;
     timed(c, "demodulation", st, [&] { launch_demod(A, D, st); });
     for (int level = 0; level < 4; ++level) timed(c, "denoise", st, [&] { launch_denoise(A, D, level, st); });
-    if (async) {
-        HK_HIP(c, hipEventRecord(c->ev_dn[c->dn_k & 1u], st));
-        HK_HIP(c, hipEventRecord(c->ev_dn_last, st));
-        c->dn_k++;
-        c->dn_pending = true;
-    }
-    c->rf_swapped = false;
-    c->dn_frame = async;
+    if (async) HK_TRY(tail_end(c));
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -1131,10 +1151,11 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     if (rc) return rc;
     if (!settings) return fail(c, HK_ERR_INVALID, "null settings");
     (void)hipSetDevice(c->device);
-    // after a denoise queued on dn_stream, the tone-sum of that frame follows it there
-    const bool async = c->dn_frame && settings->denoise;
+    // after a slot-swapping hk_render_frame: on dn_stream (after that frame's denoise, if any)
+    const bool async = c->rf_swapped;
     hipStream_t st = async ? c->dn_stream : pick(c, stream);
-    if (!async) HK_TRY(gb_join(c, st));
+    if (async) HK_TRY(tail_begin(c));
+    else HK_TRY(gb_join(c, st));
     hk_frame_inputs dummy;
     std::memset(&dummy, 0, sizeof(dummy));
     FrameArgs A = frame_args(c, settings, &dummy);
@@ -1144,11 +1165,7 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     T.indirect = settings->indirect_bounces == 0u ? nullptr : (settings->denoise ? c->denoised[2] : c->render[2]);
     T.output = c->tone_buf[c->head];
     timed(c, "tone_mapping", st, [&] { launch_tone(A, T, st); });
-    if (async) {
-        HK_HIP(c, hipEventRecord(c->ev_dn[(c->dn_k - 1u) & 1u], st));
-        HK_HIP(c, hipEventRecord(c->ev_dn_last, st));
-    }
-    c->dn_frame = false;
+    if (async) HK_TRY(tail_end(c));
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }

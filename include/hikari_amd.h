@@ -29,9 +29,14 @@
  * Conventions: every function returns 0 on success and a negative HK_ERR_* code on
  * failure; `hk_last_error` returns the message.  No exceptions cross the ABI.  A context
  * is externally synchronized (single-threaded, like one render-graph node).  `stream` is
- * a hipStream_t (NULL = the context's own stream); all GPU work is enqueued on it and
+ * a hipStream_t (NULL = the context's own stream); all GPU work is ordered on it and
  * the functions return without waiting, except hk_get_output(..., to_host=1) and
- * hk_read_counters.
+ * hk_read_counters.  Internally a frame's G-buffer and its tail (denoise, tone-sum) may run
+ * on the context's own streams, overlapping the neighbouring frames' light passes; every
+ * call that reads or changes their results first waits for them on `stream`
+ * (hipStreamWaitEvent), so the observable order is the stream order.  A host-side
+ * hipStreamSynchronize(stream) therefore does not cover them: use a readback call, or
+ * hipDeviceSynchronize.
  */
 #ifndef HIKARI_AMD_H
 #define HIKARI_AMD_H
