@@ -194,10 +194,19 @@ int tail_end(hk_ctx* c)
     c->dn_pending = true;
     return HK_OK;
 }
-bool dn_pipeline_enabled()
+// Frame pipelining pays on large frames only: on a small band or stripe (a 2- to 8-way split of
+// 1080p: <= 1 Mpx, 0.15-0.35 ms frames) the cross-stream waits cost more than the overlap hides
+// (cornell 8-way stripe 0.145 -> 0.172 ms), on a 1080p frame or a 4K band it gains.
+bool pipeline_size(const hk_ctx* c)
 {
-    static const bool on = !getenv("HK_DN_PIPELINE") || getenv("HK_DN_PIPELINE")[0] != '0';
-    return on;
+    const char* e = getenv("HK_PIPELINE_MIN_PX");  // read per call: tests switch it per context
+    const double min_px = e ? atof(e) : 1.2e6;
+    return (double)c->s[0] * (double)c->s_rows >= min_px;
+}
+bool dn_pipeline_enabled(const hk_ctx* c)
+{
+    const char* e = getenv("HK_DN_PIPELINE");
+    return (!e || e[0] != '0') && pipeline_size(c);
 }
 // the scene, sizes or G-buffer planes change on the caller's stream: the next k_gbuffer must run
 // in caller-stream order (and a synchronous change waits for the one in flight)
@@ -474,6 +483,10 @@ int hk_create(int device, hk_ctx** out)
         delete c;
         return HK_ERR_HIP;
     }
+    // side[1] runs the indirect chain.  side[0] carries no work but is kept: streams are mapped
+    // round-robin onto the process's hardware queues (GPU_MAX_HW_QUEUES = 4), and without it the
+    // G-buffer / tail streams land on queues that serialise them behind the light passes
+    // (cornell 1080p 0.601 -> 0.674 ms/frame measured without it)
     for (int k = 0; k < 2; ++k)
         if (hipStreamCreateWithFlags(&c->side[k], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming) != hipSuccess) {
@@ -947,11 +960,12 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     // passes, denoise, tone-sum, readbacks) and a post-process of frame f-1 (it reads the previous
     // slot); k_gbuffer waits for exactly those on gb_stream and so overlaps frame f-1's light
     // passes.  A scene / size / plane change since the last call serialises it instead.
-    static const bool pipeline = !getenv("HK_GB_PIPELINE") || getenv("HK_GB_PIPELINE")[0] != '0';
+    const char* gp = getenv("HK_GB_PIPELINE");
+    const bool pipeline = !gp || gp[0] != '0';
     const uint32_t e = c->gb_calls & 1u;
     HK_HIP(c, hipEventRecord(c->ev_gb_call[e], st));
     hipStream_t gs = st;
-    if (pipeline && !c->gb_serial && c->gb_calls > 0) {
+    if (pipeline && pipeline_size(c) && !c->gb_serial && c->gb_calls > 0) {
         gs = c->gb_stream;
         HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[e ^ 1u], 0));
         HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_done, 0));  // the previous k_gbuffer (if it ran on st)
@@ -1049,7 +1063,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // Frame-tail pipelining: with all three channels rendered, this frame's render / variance
     // targets are the other slot, last read by frame f-2's denoise / tone-sum, so frame f-1's tail
     // (on dn_stream) can still be running while this frame's light passes start.
-    const bool swap = dn_pipeline_enabled() && settings->indirect_bounces >= 1u;
+    const bool swap = dn_pipeline_enabled(c) && settings->indirect_bounces >= 1u;
     // (k_albedo rewrites the albedo plane a previous tail may still read: full join then)
     HK_TRY(gb_join(c, st, !swap || !c->albedo_fresh));
     if (swap) {

@@ -110,6 +110,35 @@ def test_full_size_bench_workloads_bit_exact(config, frames):
     assert r.counters() == o.counters()
 
 
+@pytest.mark.parametrize("denoise", [True, False], ids=["denoise", "tone_only"])
+def test_frame_pipelining_bit_exact(monkeypatch, denoise):
+    """Frame pipelining forced on a small frame (HK_PIPELINE_MIN_PX=0): the G-buffer of frame f on
+    its own stream next to frame f-1's light passes, frame f's tail (denoise, tone-sum) next to
+    frame f+1's; every plane, reservoir and counter of every frame as the oracle's serial run,
+    with readbacks after each frame and without (outputs compared after the last frame only)."""
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    monkeypatch.setenv("HK_PIPELINE_MIN_PX", "0")
+    w, h = 96, 72
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=denoise)
+    scene, cam, lights, r, o = _setup(w, h, st)
+    s = st.to_c()
+    errors = []
+    frames = 9
+    for f in range(frames):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        if f < 3 or f == frames - 1:  # frames 3..7 run back to back, no readback in between
+            _compare_frame(r, o, f, errors)
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
+    assert r.counters() == o.counters()
+
+
 def test_fallback_paths_bit_exact(monkeypatch):
     """The paths the defaults switch off stay exact: one stream (no channel fork), walk nodes
     without leaf collapse, the G-buffer stack with its scratch overflow levels."""
@@ -483,12 +512,16 @@ def test_gpu_instance_update_matches_host_rebuild(scene_fn):
     assert not errors, "\n".join(errors[:10])
 
 
-@pytest.mark.parametrize("ratio_setting,taa", [("SMAA_TU_2_0", "Jasmine"), ("SMAA_TU_1_0", "Jasmine"),
-                                               ("SMAA_TU_2_0", "None_")])
-def test_post_process_smaa_taa_bit_exact(ratio_setting, taa):
+@pytest.mark.parametrize("ratio_setting,taa,pipelined", [("SMAA_TU_2_0", "Jasmine", False), ("SMAA_TU_1_0", "Jasmine", False),
+                                                         ("SMAA_TU_2_0", "None_", False), ("SMAA_TU_1_0", "Jasmine", True)])
+def test_post_process_smaa_taa_bit_exact(ratio_setting, taa, pipelined, monkeypatch):
     """SMAA TU4x + TAA Jasmine (hk_post_process) on the GPU vs the oracle, bit for bit, over
-    frames with both jitter parities (the reference default pipeline is SMAA_TU_2_0 + Jasmine)."""
+    frames with both jitter parities (the reference default pipeline is SMAA_TU_2_0 + Jasmine).
+    `pipelined`: frame pipelining forced on (the post-process reads the previous G-buffer slot,
+    which the next frame's G-buffer overwrites)."""
     from hikari_amd import HikariSettings, Taa, Upscale, _abi, frame_inputs
+    if pipelined:
+        monkeypatch.setenv("HK_PIPELINE_MIN_PX", "0")
     w, h = 62, 41
     st = HikariSettings(upscale=getattr(Upscale, ratio_setting), taa=getattr(Taa, taa))
     scene, cam, lights, r, o = _setup(w, h, st)
