@@ -134,6 +134,8 @@ struct hk_ctx {
 
     // timing
     bool timing = false;
+    uint32_t timing_every = 1;   // time frames with frame_number % timing_every == 0
+    bool timing_frame = true;    // the current frame is one of them
     std::vector<TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
     std::vector<std::string> timing_names;
@@ -286,7 +288,7 @@ hipEvent_t take_event(hk_ctx* c)
 template <typename F>
 void timed(hk_ctx* c, const char* name, hipStream_t st, F&& launch)
 {
-    if (!c->timing) {
+    if (!c->timing || !c->timing_frame) {
         launch();
         return;
     }
@@ -985,6 +987,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     std::swap(c->albedo, c->albedo_prev);
     c->gslot ^= 1u;
     c->head = in->frame_number & 1u;
+    c->timing_frame = in->frame_number % c->timing_every == 0u;
     FrameArgs A = frame_args(c, nullptr, in);
     ViewArgs V;
     for (int i = 0; i < 3; ++i) V.world_position[i] = in->view.world_position[i];
@@ -1079,6 +1082,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
         return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     c->head = in->frame_number & 1u;
+    c->timing_frame = in->frame_number % c->timing_every == 0u;
     FrameArgs A = frame_args(c, settings, in);
     // The indirect channel owns reservoir buffers 6-9 (light.rs:518-546 pairs (6,8)); direct and
     // emissive share the spatial pair 4/5 and stay in reference order.  So the indirect chain can
@@ -1435,6 +1439,13 @@ int hk_enable_kernel_timing(hk_ctx* c, int enable)
     c->timing_names.clear();
     c->timing_ms.clear();
     c->timing_n.clear();
+    return HK_OK;
+}
+
+int hk_set_kernel_timing_interval(hk_ctx* c, uint32_t every)
+{
+    if (!c || every == 0) return HK_ERR_INVALID;
+    c->timing_every = every;
     return HK_OK;
 }
 

@@ -159,6 +159,7 @@ def lib() -> C.CDLL:
         "hk_read_counters": (i32, [vp, C.POINTER(hk_counters), vp]),
         "hk_enable_kernel_timing": (i32, [vp, i32]),
         "hk_kernel_timing": (i32, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), i32]),
+        "hk_set_kernel_timing_interval": (i32, [vp, u32]),
         "hk_trace": (i32, [vp, vp, vp, vp, vp, u32, vp, i32, vp]),
         "hk_selftest_f16": (i32, [vp, vp, u32, vp]),
         "hk_selftest_div": (i32, [vp, C.c_float, u32, u32, C.POINTER(C.c_uint64)]),
@@ -185,7 +186,7 @@ EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
     "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_dump_reservoirs",
-    "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing",
+    "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing", "hk_set_kernel_timing_interval",
     "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hk_selftest_rcp", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",
     "hks_add_instance", "hks_build", "hks_get_desc",
 ]

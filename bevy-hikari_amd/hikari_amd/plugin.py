@@ -170,6 +170,10 @@ class HikariRenderer:
     def enable_kernel_timing(self, enable: bool = True) -> None:
         _check(self.ctx, self._L.hk_enable_kernel_timing(self.ctx, int(enable)), "hk_enable_kernel_timing")
 
+    def set_kernel_timing_interval(self, every: int) -> None:
+        """Time only frames whose frame_number % every == 0 (hk_set_kernel_timing_interval)."""
+        _check(self.ctx, self._L.hk_set_kernel_timing_interval(self.ctx, int(every)), "hk_set_kernel_timing_interval")
+
     def kernel_timing(self) -> dict:
         names = (C.c_char_p * 64)()
         ms = (C.c_float * 64)()

@@ -270,6 +270,9 @@ int hk_read_counters(hk_ctx* ctx, hk_counters* out, void* stream);
 /* mean duration (ms) of each kernel of the last hk_render_frame/hk_denoise call, if timing is enabled */
 int hk_enable_kernel_timing(hk_ctx* ctx, int enable);
 int hk_kernel_timing(hk_ctx* ctx, const char** names, float* ms, int capacity);
+/* time only frames whose frame_number % every == 0 (default 1: every frame), so the timing
+ * events of a long measured run do not perturb most of its frames */
+int hk_set_kernel_timing_interval(hk_ctx* ctx, uint32_t every);
 
 /* ---- stand-alone ray query (minimum slice: light.wgsl:442-486) ----
  * rays: n records of {origin xyz, direction xyz} (6 floats, host or device memory)
