@@ -160,6 +160,12 @@ int fail(hk_ctx* c, int code, const std::string& msg)
 
 hipStream_t pick(hk_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
 
+// experiment switch: 0 = G-buffer and tail streams of their own, 1 = the G-buffer on side[0],
+// 2 = the tail on side[0]
+#ifndef HK_STREAM_LAYOUT
+#define HK_STREAM_LAYOUT 0
+#endif
+
 #define HK_TRY(expr)            \
     do {                        \
         int _r = (expr);        \
@@ -496,12 +502,14 @@ int hk_create(int device, hk_ctx** out)
             return HK_ERR_HIP;
         }
     if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking) != hipSuccess ||
+        (HK_STREAM_LAYOUT == 1 ? (c->gb_stream = c->side[0], hipSuccess)
+                               : hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking)) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking) != hipSuccess ||
+        (HK_STREAM_LAYOUT == 2 ? (c->dn_stream = c->side[0], hipSuccess)
+                               : hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking)) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rf, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rslot[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rslot[1], hipEventDisableTiming) != hipSuccess ||
@@ -549,8 +557,8 @@ void hk_destroy(hk_ctx* c)
     for (hipEvent_t e : {c->ev_gb_done, c->ev_gb_call[0], c->ev_gb_call[1], c->ev_post, c->ev_rf, c->ev_rslot[0],
                          c->ev_rslot[1], c->ev_gslot[0], c->ev_gslot[1], c->ev_dn_last})
         if (e) (void)hipEventDestroy(e);
-    if (c->gb_stream) (void)hipStreamDestroy(c->gb_stream);
-    if (c->dn_stream) (void)hipStreamDestroy(c->dn_stream);
+    if (c->gb_stream && c->gb_stream != c->side[0]) (void)hipStreamDestroy(c->gb_stream);
+    if (c->dn_stream && c->dn_stream != c->side[0]) (void)hipStreamDestroy(c->dn_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
