@@ -309,6 +309,27 @@ def main():
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         rays = int(n.item())
 
+    # after the timed region: a few frames with every kernel alone on the GPU (no channel fork, no
+    # frame pipelining), so the roofline can also quote the dominant kernel's isolated duration
+    isolated = None
+    if world == 1 and spp == 1 and not dynamic:
+        iso_env = {"HK_CHANNEL_STREAMS": "0", "HK_GB_PIPELINE": "0", "HK_DN_PIPELINE": "0"}
+        saved = {k: os.environ.get(k) for k in iso_env}
+        os.environ.update(iso_env)
+        r.set_kernel_timing_interval(1)
+        r.enable_kernel_timing(True)
+        f0 = args.warmup + args.steps
+        for f in range(f0, f0 + 8):
+            step(f)
+        torch.cuda.synchronize()
+        isolated = r.kernel_timing()
+        r.enable_kernel_timing(False)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         mrays = rays / elapsed / 1e6
@@ -351,6 +372,12 @@ def main():
                          "frame_frac": round(frame_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
         }
+        if isolated and dom in isolated:
+            # the same kernel with the GPU to itself (8 untimed frames after the timed region)
+            iso = isolated[dom]
+            result["roofline"]["isolated_avg_ms"] = round(iso, 4)
+            result["roofline"]["isolated_achieved"] = round(alg / (iso * 1e-3) / 1e9, 1)
+            result["roofline"]["isolated_frac"] = round(alg / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         tb = load_traversal_bytes(args.config) if world == 1 and spp == 1 else None
         if tb is not None:
             # §8d's second component: node / triangle / instance / hit_info bytes of the light passes
