@@ -370,6 +370,29 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     wave_count(A.cnt.emitter, n_emitter);
 }
 
+// direct_lit alone (no emissive sampling) fits 128 VGPRs with at most a few scratch words: the
+// same body with 4 waves per SIMD for the separate-launch path (bands / stripes) when the grid
+// has enough waves to use them (>= 400 K pixels): cornell 2-way stripe 0.348 -> 0.328 ms/frame,
+// 4-way 0.192 -> 0.187; an 8-way stripe (259 K pixels, about one wave per slot) 0.1455 -> 0.1474
+#ifndef HK_DIRECT_LIT_W4
+#define HK_DIRECT_LIT_W4 1
+#endif
+constexpr size_t DIRECT_LIT_W4_MIN_PX = 400000;
+template <bool LDS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_lit_w4(FrameArgs A, ChannelArgs C)
+{
+    Scene sc;
+    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+    else sc = A.sc;
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+        direct_body<false, true>(A, sc, C, x, y, n_top, n_emitter);
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
 // direct_lit then the emissive pass in one launch, each thread running both passes for its pixel
 // in the reference's pass order.  Both passes store into the spatial reservoir pair they share
 // only at their own pixel when the reprojection is the identity (zero velocity at upscale ratio
@@ -965,7 +988,10 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
         if (lds) hipLaunchKernelGGL((k_direct<true, false, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_direct<true, false, false>), g, dim3(256), 0, st, A, C);
     } else {
-        if (lds) hipLaunchKernelGGL((k_direct<false, true, true>), g, dim3(256), lds, st, A, C);
+        if (HK_DIRECT_LIT_W4 && (size_t)A.F.s[0] * (size_t)A.F.s_rows >= DIRECT_LIT_W4_MIN_PX) {
+            if (lds) hipLaunchKernelGGL(k_direct_lit_w4<true>, g, dim3(256), lds, st, A, C);
+            else hipLaunchKernelGGL(k_direct_lit_w4<false>, g, dim3(256), 0, st, A, C);
+        } else if (lds) hipLaunchKernelGGL((k_direct<false, true, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_direct<false, true, false>), g, dim3(256), 0, st, A, C);
     }
 }
