@@ -135,6 +135,25 @@ HKD float ndc_depth(const float* vp, f3 p)
     f4 c = mat4_mul(vp, mk4(p.x, p.y, p.z, 1.0f));
     return c.z / c.w;
 }
+// utils.wgsl:30-35
+HKD f2 clip_to_uv(f4 clip)
+{
+    f2 uv = mk2(clip.x / clip.w, clip.y / clip.w);
+    uv = mk2((uv.x + 1.0f) * 0.5f, (uv.y + 1.0f) * 0.5f);
+    return mk2(uv.x, 1.0f - uv.y);
+}
+// prepass.wgsl:49-50,96: the hit's object-space point p (the triangle's barycentric combination,
+// what the rasteriser interpolates) through this frame's model and view and the previous ones
+HKD f2 motion_vector(const ViewArgs& V, const hk_instance& in, uint32_t instance, f3 t0, f3 t1, f3 t2, f2 bary)
+{
+    const f3 lp = (t0 + (t1 - t0) * bary.x) + (t2 - t0) * bary.y;
+    const f4 l4 = mk4(lp.x, lp.y, lp.z, 1.0f);
+    const f4 wc = mat4_mul(in.model, l4);
+    const f4 wp = mat4_mul(V.previous_models + 16u * (size_t)instance, l4);
+    const f2 a = clip_to_uv(mat4_mul(V.view_proj, wc));
+    const f2 b = clip_to_uv(mat4_mul(V.previous_view_proj, wp));
+    return mk2(a.x - b.x, a.y - b.y);
+}
 
 extern __shared__ uint32_t hk_lds_scene[];
 
@@ -170,7 +189,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
         int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
         Ray ray;
         ray.origin = ld3(V.world_position);
-        ray.direction = primary_direction(V, (float)x + 0.5f, (float)y + 0.5f, A.F.S);
+        ray.direction = primary_direction(V, ((float)x + 0.5f) - V.jitter[0], ((float)y + 0.5f) - V.jitter[1], A.F.S);
         ray.inv_direction = inv(ray.direction);
         Hit hit = closest_hit_ordered<SHALLOW && !LDS>(sc, ray, LDS ? nullptr : gb_lds_stack);
         if (hit.instance_index == HK_U32_MAX) {
@@ -200,8 +219,8 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
             float grad[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-                f3 d = primary_direction(V, (float)x + 0.5f + (k == 0 ? 1.0f : 0.0f),
-                                         (float)y + 0.5f + (k == 1 ? 1.0f : 0.0f), A.F.S);
+                f3 d = primary_direction(V, ((float)x + 0.5f + (k == 0 ? 1.0f : 0.0f)) - V.jitter[0],
+                                         ((float)y + 0.5f + (k == 1 ? 1.0f : 0.0f)) - V.jitter[1], A.F.S);
                 float denom = dot(d, ng);
                 grad[k] = 0.0f;
                 if (denom != 0.0f) {
@@ -211,7 +230,9 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
             }
             A.G.depth_gradient[idx] = make_float2(grad[0], grad[1]);
             A.G.instance_material[idx] = make_float2((float)hit.instance_index + 0.5f, (float)info.material_index + 0.5f);
-            A.G.velocity_uv[idx] = make_float4(0.0f, 0.0f, info.uv.x, info.uv.y);
+            f2 velocity = mk2(0.0f, 0.0f);  // exactly what motion_vector gives when nothing moved
+            if (V.motion) velocity = motion_vector(V, in, hit.instance_index, t0, t1, t2, hit.uv);
+            A.G.velocity_uv[idx] = make_float4(velocity.x, velocity.y, info.uv.x, info.uv.y);
         }
     }
     if (y < A.F.count_Sy0 || y >= A.F.count_Sy1) n_primary = 0;
@@ -988,7 +1009,9 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
         if (lds) hipLaunchKernelGGL((k_direct<true, false, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_direct<true, false, false>), g, dim3(256), 0, st, A, C);
     } else {
-        if (HK_DIRECT_LIT_W4 && (size_t)A.F.s[0] * (size_t)A.F.s_rows >= DIRECT_LIT_W4_MIN_PX) {
+        const char* wmin = getenv("HK_DIRECT_W4_MIN_PX");  // read per launch: tests force either kernel
+        const double w4_min = wmin ? atof(wmin) : (double)DIRECT_LIT_W4_MIN_PX;
+        if (HK_DIRECT_LIT_W4 && (double)A.F.s[0] * (double)A.F.s_rows >= w4_min) {
             if (lds) hipLaunchKernelGGL(k_direct_lit_w4<true>, g, dim3(256), lds, st, A, C);
             else hipLaunchKernelGGL(k_direct_lit_w4<false>, g, dim3(256), 0, st, A, C);
         } else if (lds) hipLaunchKernelGGL((k_direct<false, true, true>), g, dim3(256), lds, st, A, C);

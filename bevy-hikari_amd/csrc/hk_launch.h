@@ -32,6 +32,13 @@ struct ViewArgs {
     float world_position[3];
     float view_proj[16];
     float inverse_view_proj[16];
+    // prepass.wgsl:30-54: the primary ray of pixel (x, y) goes through (x + 0.5 - jitter[0], y + 0.5 - jitter[1])
+    float jitter[2];
+    // motion vectors (prepass.wgsl:96): 0 = camera and every instance static this frame, so the
+    // velocity is exactly zero and is not computed
+    int motion;
+    float previous_view_proj[16];
+    const float* previous_models;  // 16 floats per instance: model at the previous k_gbuffer
 };
 
 // All channels of one frame (post_process.rs:1199-1223 runs them one after another).

@@ -49,6 +49,11 @@ struct hk_ctx {
     uint32_t gb_blas_depth = 0;   // BLAS part of it (the TLAS part changes with hk_update_instances)
     void* dyn_scratch = nullptr;  // hk_update_instances scratch (sized at upload)
     size_t dyn_bytes = 0;
+    // GlobalTransformQueue[1] of every instance (transform.rs:32-44): the models as of the previous
+    // k_gbuffer, read by its motion vectors; refreshed after a k_gbuffer that followed an update
+    float* prev_models = nullptr;
+    bool models_dirty = false;   // hk_update_instances ran since the last k_gbuffer
+    bool velocity_zero = true;   // the current G-buffer's velocity plane is all zero (k_gbuffer, no motion)
     bool has_scene = false;
     uchar4* noise = nullptr;
     bool has_noise = false;
@@ -538,6 +543,7 @@ void hk_destroy(hk_ctx* c)
     release(c->walk_nodes[1]);
     release(c->collapse_scratch);
     release(c->dyn_scratch);
+    release(c->prev_models);
     release(c->tex_desc);
     release(c->texels);
     release(c->tex_lut);
@@ -663,6 +669,12 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
         launch_collapse_leaves(c->walk_nodes[1], n_tlas, nullptr, nullptr, c->collapse_scratch, c->stream);
     }
     HK_HIP(c, hipGetLastError());
+    // previous models = the uploaded ones (GlobalTransformQueue([matrix; 2]) for a new entity)
+    release(c->prev_models);
+    HK_HIP(c, hipMalloc(&c->prev_models, (size_t)d->instances.count * 64));
+    HK_HIP(c, hipMemcpy2DAsync(c->prev_models, 64, (const char*)c->buf[4] + offsetof(hk_instance, model),
+                               sizeof(hk_instance), 64, d->instances.count, hipMemcpyDeviceToDevice, c->stream));
+    c->models_dirty = false;
     HK_HIP(c, hipStreamSynchronize(c->stream));
     release(d_aux);
     c->has_scene = true;
@@ -739,6 +751,7 @@ int hk_update_instances(hk_ctx* c, const float* models, const float* local_aabbs
     HK_HIP(c, hipStreamSynchronize(st));
     if (flags[0]) return fail(c, HK_ERR_INVALID, "singular instance transform");
     c->gb_stack_need = flags[1] + c->gb_blas_depth;
+    c->models_dirty = true;  // the next G-buffer reads the models before this update as the previous ones
     return HK_OK;
 }
 
@@ -963,6 +976,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     if (!in) return fail(c, HK_ERR_INVALID, "null frame inputs");
     if (c->gb_stack_need > (uint32_t)GB_STACK)
         return fail(c, HK_ERR_INVALID, "scene BVH too deep for the G-buffer traversal stack (TLAS + BLAS depth > 64)");
+    if (in->jitter > HK_JITTER_TAA_SMAA) return fail(c, HK_ERR_INVALID, "unknown jitter mode");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
     // Pipelining: this frame's planes go to the slot frame f-2 used.  Its readers are the work
@@ -1001,9 +1015,35 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     for (int i = 0; i < 3; ++i) V.world_position[i] = in->view.world_position[i];
     std::memcpy(V.view_proj, in->view.view_proj, sizeof(V.view_proj));
     std::memcpy(V.inverse_view_proj, in->view.inverse_view_proj, sizeof(V.inverse_view_proj));
+    // prepass.wgsl:30-38 frame_jitter (HALTON, view.rs:130-139), in pixels (jitter = 2 h / viewport
+    // in NDC, added to clip.xy with y flipped: the surface point seen at a pixel centre c is the one
+    // that projects to c - h without jitter)
+    static const float HALTON[8][4] = {
+        {0.000000f, 0.000000f, 0.500000f, 0.333333f}, {0.250000f, 0.666667f, 0.750000f, 0.111111f},
+        {0.125000f, 0.444444f, 0.625000f, 0.777778f}, {0.375000f, 0.222222f, 0.875000f, 0.555556f},
+        {0.062500f, 0.888889f, 0.562500f, 0.037037f}, {0.312500f, 0.370370f, 0.812500f, 0.703704f},
+        {0.187500f, 0.148148f, 0.687500f, 0.481481f}, {0.437500f, 0.814815f, 0.937500f, 0.259259f}};
+    V.jitter[0] = V.jitter[1] = 0.0f;
+    if (in->jitter != HK_JITTER_NONE) {
+        const uint32_t index = in->jitter == HK_JITTER_TAA_SMAA ? (in->frame_number >> 1) & 15u : in->frame_number & 15u;
+        const float* h = HALTON[index >> 1];
+        V.jitter[0] = (index & 1u) == 0u ? h[0] : h[2];
+        V.jitter[1] = (index & 1u) == 0u ? h[1] : h[3];
+    }
+    // motion vectors: previous view (PreviousViewUniform) and previous models (GlobalTransformQueue)
+    const float* pvp = in->has_previous_view ? in->previous_view_proj : in->view.view_proj;
+    std::memcpy(V.previous_view_proj, pvp, sizeof(V.previous_view_proj));
+    V.motion = (c->models_dirty || std::memcmp(pvp, in->view.view_proj, sizeof(V.previous_view_proj)) != 0) ? 1 : 0;
+    V.previous_models = c->prev_models;
     // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
     // hk_render_frame runs it on its own only for host-supplied G-buffers
     timed(c, "gbuffer", gs, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, gs); });
+    if (c->models_dirty) {  // this frame's models become the next frame's previous ones
+        HK_HIP(c, hipMemcpy2DAsync(c->prev_models, 64, (const char*)c->buf[4] + offsetof(hk_instance, model),
+                                   sizeof(hk_instance), 64, c->count[4], hipMemcpyDeviceToDevice, gs));
+        c->models_dirty = false;
+    }
+    c->velocity_zero = V.motion == 0;
     HK_HIP(c, hipEventRecord(c->ev_gb_done, gs));
     if (gs != st) c->gb_pending = true;
     c->gb_serial = false;
@@ -1109,12 +1149,17 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (!c->albedo_fresh) timed(c, "full_screen_albedo", st, [&] { launch_albedo(A, c->albedo, st); });
     ChannelArgs C0 = channel(c, A.F.number, 0);
     ChannelArgs C1 = channel(c, A.F.number, 1);
-    // direct_lit + emissive in one launch when every reprojection is the identity (k_gbuffer's
-    // zero velocity at ratio 1): see k_direct_fused.  Only for frames of >= 1 Mpx: there it saves
-    // a launch and a tail (cornell 1080p 0.652 -> 0.622 ms); on a small band (a 4- or 8-way
-    // split) the two passes on their own overlap the indirect chain better (0.143 vs 0.151 ms).
-    const bool fuse = c->albedo_fresh && c->ratio == 1.0f && (size_t)c->s[0] * (size_t)c->s_rows >= (1u << 20) &&
-                      !getenv("HK_NO_FUSE");
+    // direct_lit + emissive in one launch when every reprojection is the identity: see
+    // k_direct_fused.  That needs a zero velocity plane (k_gbuffer of a frame without camera or
+    // instance motion: velocity_zero; host planes may hold any velocity) at upscale ratio 1 (the
+    // deferred jitter is the identity).  Only for frames of >= 1 Mpx: there it saves a launch and a
+    // tail (cornell 1080p 0.652 -> 0.622 ms); on a small band (a 4- or 8-way split) the two passes
+    // on their own overlap the indirect chain better (0.143 vs 0.151 ms).  HK_FUSE_MIN_PX overrides
+    // the size threshold (tests).
+    const char* fmin = getenv("HK_FUSE_MIN_PX");
+    const double fuse_min_px = fmin ? atof(fmin) : (double)(1u << 20);
+    const bool fuse = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f &&
+                      (double)c->s[0] * (double)c->s_rows >= fuse_min_px && !getenv("HK_NO_FUSE");
     if (fuse) {
         timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(A, C0, C1, st); });
     } else {
@@ -1339,6 +1384,13 @@ const void* hk_output_device_ptr(hk_ctx* c, int id)
 {
     if (!c || !c->sized) return nullptr;
     return output_ptr(c, id, nullptr, nullptr, nullptr);
+}
+
+int hk_sync(hk_ctx* c, void* stream)
+{
+    if (!c) return HK_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    return gb_join(c, pick(c, stream));
 }
 
 int hk_get_output(hk_ctx* c, int id, void* dst, size_t bytes, int to_host, void* stream)

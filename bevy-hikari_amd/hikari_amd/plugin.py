@@ -145,7 +145,19 @@ class HikariRenderer:
         return out
 
     def output_device_ptr(self, output_id: int) -> int:
+        """Device address of the plane for this frame (call sync(stream) before reading it there)."""
         return self._L.hk_output_device_ptr(self.ctx, output_id)
+
+    def sync(self, stream=None) -> None:
+        """`stream` waits for the context's own streams (hk_sync)."""
+        _check(self.ctx, self._L.hk_sync(self.ctx, stream), "hk_sync")
+
+    def set_gbuffer_plane(self, plane: int, data: np.ndarray, stream=None) -> None:
+        """A host G-buffer plane (hk_set_gbuffer_plane; 0..4 = position, normal, depth gradient,
+        instance/material, velocity/uv), the route that keeps the reference's raster prepass."""
+        d = np.ascontiguousarray(data)
+        _check(self.ctx, self._L.hk_set_gbuffer_plane(self.ctx, plane, d.ctypes.data, d.nbytes, 0, stream),
+               "hk_set_gbuffer_plane")
 
     def reservoirs(self, buffer_id: int) -> np.ndarray:
         w, h, _ = self.output_info(_abi.OUT_VARIANCE[0])
@@ -225,15 +237,23 @@ class HikariPlugin:
         if self.universal.build_mesh_acceleration_structure and self.universal.build_instance_acceleration_structure:
             self.renderer.upload_scene(scene)
         self.frame_number = 0
+        self._previous_camera = None
 
     def resize(self, width: int, height: int, band_y0: int = 0, band_rows: int = 0):
         self.renderer.resize(width, height, self.settings.upscale.ratio(), band_y0, band_rows)
 
     def frame(self, camera, lights, gbuffer: bool = True, stream=None) -> None:
-        from .scene import frame_inputs
+        """One frame.  The previous frame's camera is the PreviousViewUniform of the motion vectors
+        (view.rs:47-73; the first frame has none: static) and the prepass jitters the primary rays
+        when TAA is on (prepass.rs:194-199)."""
+        import copy
+
+        from .scene import frame_inputs, jitter_mode
         r = self.renderer
         s = self.settings.to_c()
-        fi = frame_inputs(self.frame_number, camera, lights, r.width, r.height)
+        fi = frame_inputs(self.frame_number, camera, lights, r.width, r.height,
+                          previous_camera=self._previous_camera, jitter=jitter_mode(self.settings))
+        self._previous_camera = copy.deepcopy(camera)
         if gbuffer:
             r.render_gbuffer(fi, stream)
         r.render_frame(s, fi, stream)

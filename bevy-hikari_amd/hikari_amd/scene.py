@@ -170,11 +170,28 @@ def make_lights(directional: Optional[DirectionalLight], ambient: AmbientLight =
     return L
 
 
-def frame_inputs(number: int, camera: Camera, lights: _abi.hk_lights, width: int, height: int) -> _abi.hk_frame_inputs:
+def jitter_mode(settings) -> int:
+    """The prepass shader defs of HikariSettings (prepass.rs:194-199): TEMPORAL_ANTI_ALIASING when
+    taa is Jasmine, plus SMAA_TU4X when the upscaler is SMAA TU4x."""
+    if settings.taa.value != 0:
+        return _abi.JITTER_NONE
+    return _abi.JITTER_TAA_SMAA if settings.upscale.kind == "SmaaTu4x" else _abi.JITTER_TAA
+
+
+def frame_inputs(number: int, camera: Camera, lights: _abi.hk_lights, width: int, height: int,
+                 previous_camera: Optional[Camera] = None, jitter: int = 0) -> _abi.hk_frame_inputs:
+    """hk_frame_inputs of frame `number`.  previous_camera: the camera of the previous frame
+    (PreviousViewUniform, view.rs:47-73; None = a static camera); jitter: hk_frame_inputs.jitter."""
     f = _abi.hk_frame_inputs()
     f.frame_number = int(number)
+    f.jitter = int(jitter)
     f.view = camera.view(width, height)
     f.lights = lights
+    if previous_camera is not None:
+        f.has_previous_view = 1
+        pv = previous_camera.view(width, height)
+        for i in range(16):
+            f.previous_view_proj[i] = pv.view_proj[i]
     return f
 
 

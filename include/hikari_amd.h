@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HK_ABI_VERSION 1
+#define HK_ABI_VERSION 2
 
 enum {
     HK_OK = 0,
@@ -125,12 +125,26 @@ typedef struct hk_lights {
     float ambient_color[4];         /* lights.ambient_color */
 } hk_lights;
 
-/* Per-frame inputs: FrameUniform.number (view.rs:141-192) + view + lights. */
+/* Prepass sub-pixel jitter (prepass.wgsl:30-38,52-54): the shader defs the prepass pipeline gets from
+ * HikariSettings (prepass.rs:194-199) */
+enum {
+    HK_JITTER_NONE = 0, /* taa = None: no jitter */
+    HK_JITTER_TAA = 1,  /* TEMPORAL_ANTI_ALIASING: halton index = frame_number & 15 */
+    HK_JITTER_TAA_SMAA = 2, /* TEMPORAL_ANTI_ALIASING + SMAA_TU4X: index = (frame_number >> 1) & 15 */
+};
+
+/* Per-frame inputs: FrameUniform.number (view.rs:141-192) + view + lights, and the previous frame's
+ * view (`PreviousViewUniform`, view.rs:31-73: projection * inverse(GlobalTransformQueue[1])) that the
+ * prepass's motion vectors read (prepass.wgsl:96).  A zero-initialised tail (jitter 0,
+ * has_previous_view 0) means no jitter and a static camera (previous view = this view). */
 typedef struct hk_frame_inputs {
     uint32_t frame_number;
-    uint32_t _pad[3];
+    uint32_t jitter;            /* HK_JITTER_*: hk_render_gbuffer's primary-ray jitter */
+    uint32_t has_previous_view; /* 0: previous_view_proj is ignored and taken equal to view.view_proj */
+    uint32_t _pad;
     hk_view view;
     hk_lights lights;
+    float previous_view_proj[16]; /* column-major */
 } hk_frame_inputs;
 
 /* Output planes readable with hk_get_output. Sizes are per pixel of the plane's extent. */
@@ -242,6 +256,13 @@ int hk_set_band_halo(hk_ctx* ctx, uint32_t rows);
 int hk_band_info(const hk_ctx* ctx, int32_t* row0, int32_t* rows, int32_t* core_row0, int32_t* core_rows);
 
 /* ---- per frame ---- */
+/* Primary-ray G-buffer (prepass.wgsl:84-100).  Pixel (x, y) traces the ray through
+ * (x + 0.5 - jx, y + 0.5 - jy), j = the frame's halton jitter in pixels (inputs->jitter), and writes
+ * velocity = clip_to_uv(view_proj * model * p) - clip_to_uv(previous_view_proj * previous_model * p)
+ * for the hit's object-space point p (prepass.wgsl:49-50,96).  previous_model is the instance's model
+ * as of the previous hk_render_gbuffer call (GlobalTransformQueue, transform.rs:32-44; after
+ * hk_scene_upload: the uploaded model), so instances moved by hk_update_instances get motion vectors
+ * for one frame. */
 int hk_render_gbuffer(hk_ctx* ctx, const hk_frame_inputs* inputs, void* stream);
 /* plane: 0..4 = position, normal, depth_gradient, instance_material, velocity_uv
  * (full S-sized planes, or the band's rows); device_ptr != 0 => data is a device pointer */
@@ -257,7 +278,13 @@ int hk_output_info(const hk_ctx* ctx, int output_id, uint32_t* width, uint32_t* 
                    uint32_t* bytes_per_pixel);
 /* rows [row0, row0+rows) of the plane (rows = 0 => all) */
 int hk_get_output(hk_ctx* ctx, int output_id, void* dst, size_t bytes, int to_host, void* stream);
+/* Device address of an output plane for zero-copy readers.  The planes of the G-buffer, render /
+ * variance targets and albedo alternate between two slots from frame to frame, so the address is
+ * valid for the current frame only; work on `stream` sees the plane's final contents after
+ * hk_sync(ctx, stream) (the frame's G-buffer and tail may still run on the context's own streams). */
 const void* hk_output_device_ptr(hk_ctx* ctx, int output_id);
+/* Make `stream` wait (device-side) for all work the context queued on its own streams. */
+int hk_sync(hk_ctx* ctx, void* stream);
 /* copy band-local rows [row0, row0+rows) of an output plane (e.g. the band's core rows for the
  * multi-GPU all-gather); dst is host (to_host=1) or device memory */
 int hk_copy_output_rows(hk_ctx* ctx, int output_id, uint32_t row0, uint32_t rows, void* dst, int to_host,

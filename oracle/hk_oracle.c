@@ -125,6 +125,9 @@ struct hko_ctx {
     hk_material* materials; uint32_t n_materials;
     hk_node* emissive_nodes; uint32_t n_emissive_nodes;
     hk_emissive* emissives; uint32_t n_emissives;
+    /* GlobalTransformQueue[1] (transform.rs:32-44): every instance's model as of the previous
+     * hko_render_gbuffer, read by the motion vectors (prepass.wgsl:50,96) */
+    float* prev_models;
     /* material textures (hko_set_textures; none = the NO_TEXTURE pipeline) */
     hk_texture_desc* tex_desc; uint32_t* texels; uint32_t n_textures;
     float tex_lut[512];
@@ -1620,13 +1623,35 @@ static v3 primary_direction(const hk_view* view, float px, float py, const uint3
     v3 near = div3s(xyz(p), p.w);
     return normalize3(sub3(near, ld3(view->world_position)));
 }
-static void gbuffer_pixel(const hko_ctx* c, Counts* cnt, const hk_frame_inputs* in, int32_t x, int32_t y)
+/* utils.wgsl:30-35 */
+static v2 clip_to_uv(v4 clip)
+{
+    v2 uv = V2(clip.x / clip.w, clip.y / clip.w);
+    uv = V2((uv.x + 1.0f) * 0.5f, (uv.y + 1.0f) * 0.5f);
+    return V2(uv.x, 1.0f - uv.y);
+}
+/* Per-frame prepass state: the halton jitter in pixels (prepass.wgsl:30-38,52-54: jitter =
+ * 2 h / viewport in NDC added to clip.xy with y flipped, so the point seen at pixel centre c is the
+ * one that projects to c - h) and the motion-vector inputs. */
+typedef struct {
+    float jitter[2];
+    int motion;                    /* camera or any instance moved: velocities are computed */
+    const float* previous_view_proj;
+} GbFrame;
+static const float HALTON[8][4] = { /* view.rs:130-139 */
+    {0.000000f, 0.000000f, 0.500000f, 0.333333f}, {0.250000f, 0.666667f, 0.750000f, 0.111111f},
+    {0.125000f, 0.444444f, 0.625000f, 0.777778f}, {0.375000f, 0.222222f, 0.875000f, 0.555556f},
+    {0.062500f, 0.888889f, 0.562500f, 0.037037f}, {0.312500f, 0.370370f, 0.812500f, 0.703704f},
+    {0.187500f, 0.148148f, 0.687500f, 0.481481f}, {0.437500f, 0.814815f, 0.937500f, 0.259259f}};
+
+static void gbuffer_pixel(const hko_ctx* c, Counts* cnt, const hk_frame_inputs* in, const GbFrame* G, int32_t x,
+                          int32_t y)
 {
     size_t idx = (size_t)y * c->S[0] + (size_t)x;
     const hk_view* view = &in->view;
     Ray ray;
     ray.origin = ld3(view->world_position);
-    ray.direction = primary_direction(view, (float)x + 0.5f, (float)y + 0.5f, c->S);
+    ray.direction = primary_direction(view, ((float)x + 0.5f) - G->jitter[0], ((float)y + 0.5f) - G->jitter[1], c->S);
     ray.inv_direction = inv3(ray.direction);
     cnt->primary++;
     Counts dummy = {0, 0, 0};
@@ -1659,7 +1684,8 @@ static void gbuffer_pixel(const hko_ctx* c, Counts* cnt, const hk_frame_inputs* 
     float plane = dot3(sub3(p, ray.origin), ng);
     float grad[2];
     for (int k = 0; k < 2; ++k) {
-        v3 d = primary_direction(view, (float)x + 0.5f + (k == 0 ? 1.0f : 0.0f), (float)y + 0.5f + (k == 1 ? 1.0f : 0.0f), c->S);
+        v3 d = primary_direction(view, ((float)x + 0.5f + (k == 0 ? 1.0f : 0.0f)) - G->jitter[0],
+                                 ((float)y + 0.5f + (k == 1 ? 1.0f : 0.0f)) - G->jitter[1], c->S);
         float denom = dot3(d, ng);
         grad[k] = 0.0f;
         if (denom != 0.0f) {
@@ -1671,7 +1697,20 @@ static void gbuffer_pixel(const hko_ctx* c, Counts* cnt, const hk_frame_inputs* 
     gd[0] = grad[0]; gd[1] = grad[1];
     gi[0] = (float)hit.instance_index + 0.5f;
     gi[1] = (float)info.material_index + 0.5f;
-    gv[0] = 0.0f; gv[1] = 0.0f; /* static camera and scene: velocity is exactly zero */
+    /* prepass.wgsl:49-50,96: the hit's object-space point (the barycentric combination of the
+     * triangle, what the rasteriser interpolates) through this frame's and the previous frame's
+     * model and view; exactly zero when nothing moved */
+    gv[0] = 0.0f; gv[1] = 0.0f;
+    if (G->motion) {
+        v3 t0 = ld3(tv[0].position), t1 = ld3(tv[1].position), t2 = ld3(tv[2].position);
+        v3 lp = add3(add3(t0, scale3(sub3(t1, t0), hit.intersection.uv.x)), scale3(sub3(t2, t0), hit.intersection.uv.y));
+        v4 l4 = V4(lp.x, lp.y, lp.z, 1.0f);
+        v4 wc = mat4_mul(instance->model, l4);
+        v4 wp = mat4_mul(c->prev_models + 16 * (size_t)hit.instance_index, l4);
+        v2 a = clip_to_uv(mat4_mul(view->view_proj, wc)), b = clip_to_uv(mat4_mul(G->previous_view_proj, wp));
+        gv[0] = a.x - b.x;
+        gv[1] = a.y - b.y;
+    }
     gv[2] = info.uv.x; gv[3] = info.uv.y;
 }
 
@@ -1831,6 +1870,8 @@ hko_ctx* hko_create(const hk_scene_desc* sc, const uint8_t* noise, uint32_t widt
     c->materials = (hk_material*)xdup(&sc->materials, sizeof(hk_material)); c->n_materials = sc->materials.count;
     c->emissive_nodes = (hk_node*)xdup(&sc->emissive_nodes, sizeof(hk_node)); c->n_emissive_nodes = sc->emissive_nodes.count;
     c->emissives = (hk_emissive*)xdup(&sc->emissives, sizeof(hk_emissive)); c->n_emissives = sc->emissives.count;
+    c->prev_models = (float*)calloc((size_t)(c->n_instances ? c->n_instances : 1) * 16, sizeof(float));
+    for (uint32_t i = 0; i < c->n_instances; ++i) memcpy(c->prev_models + 16 * (size_t)i, c->instances[i].model, 64);
     if (noise) memcpy(c->noise, noise, sizeof(c->noise));
     if (ratio < 1.0f) ratio = 1.0f;
     if (ratio > 2.0f) ratio = 2.0f;
@@ -1896,6 +1937,7 @@ void hko_destroy(hko_ctx* c)
     if (!c) return;
     free(c->vertices); free(c->primitives); free(c->asset_nodes); free(c->alias_table); free(c->instances);
     free(c->instance_nodes); free(c->materials); free(c->emissive_nodes); free(c->emissives);
+    free(c->prev_models);
     free(c->tex_desc); free(c->texels);
     free(c->g_position); free(c->g_normal); free(c->g_depth_gradient); free(c->g_instance_material); free(c->g_velocity_uv);
     free(c->albedo);
@@ -1939,13 +1981,50 @@ void hko_render_gbuffer(hko_ctx* c, const hk_frame_inputs* in)
     c->g_velocity_uv = c->g_prev_velocity_uv;
     c->g_prev_velocity_uv = t;
     set_head(c, in->frame_number);
+    GbFrame G;
+    G.jitter[0] = G.jitter[1] = 0.0f;
+    if (in->jitter == HK_JITTER_TAA || in->jitter == HK_JITTER_TAA_SMAA) {
+        /* frame_jitter (prepass.wgsl:30-38) */
+        uint32_t index = in->jitter == HK_JITTER_TAA_SMAA ? (in->frame_number >> 1) & 15u : in->frame_number & 15u;
+        const float* h = HALTON[index >> 1];
+        G.jitter[0] = (index & 1u) == 0u ? h[0] : h[2];
+        G.jitter[1] = (index & 1u) == 0u ? h[1] : h[3];
+    }
+    G.previous_view_proj = in->has_previous_view ? in->previous_view_proj : in->view.view_proj;
+    G.motion = memcmp(G.previous_view_proj, in->view.view_proj, 64) != 0;
+    for (uint32_t i = 0; i < c->n_instances && !G.motion; ++i)
+        G.motion = memcmp(c->prev_models + 16 * (size_t)i, c->instances[i].model, 64) != 0;
 #pragma omp parallel HKO_THREADS(c)
     {
         Counts k = {0, 0, 0};
 #pragma omp for schedule(dynamic, 4)
         for (int32_t y = c->band_y0; y < c->band_y1; ++y)
-            for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) gbuffer_pixel(c, &k, in, x, y);
+            for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) gbuffer_pixel(c, &k, in, &G, x, y);
         add_counts(c, &k);
+    }
+    /* this frame's models are the next frame's previous ones */
+    for (uint32_t i = 0; i < c->n_instances; ++i) memcpy(c->prev_models + 16 * (size_t)i, c->instances[i].model, 64);
+}
+
+/* replace the scene arrays (hk_update_instances / a host rebuild); the previous models stay */
+void hko_set_scene(hko_ctx* c, const hk_scene_desc* sc)
+{
+    free(c->vertices); free(c->primitives); free(c->asset_nodes); free(c->alias_table); free(c->instances);
+    free(c->instance_nodes); free(c->materials); free(c->emissive_nodes); free(c->emissives);
+    uint32_t old_n = c->n_instances;
+    c->vertices = (hk_vertex*)xdup(&sc->vertices, sizeof(hk_vertex)); c->n_vertices = sc->vertices.count;
+    c->primitives = (hk_primitive*)xdup(&sc->primitives, sizeof(hk_primitive)); c->n_primitives = sc->primitives.count;
+    c->asset_nodes = (hk_node*)xdup(&sc->asset_nodes, sizeof(hk_node)); c->n_asset_nodes = sc->asset_nodes.count;
+    c->alias_table = (hk_alias_entry*)xdup(&sc->alias_table, sizeof(hk_alias_entry)); c->n_alias = sc->alias_table.count;
+    c->instances = (hk_instance*)xdup(&sc->instances, sizeof(hk_instance)); c->n_instances = sc->instances.count;
+    c->instance_nodes = (hk_node*)xdup(&sc->instance_nodes, sizeof(hk_node)); c->n_instance_nodes = sc->instance_nodes.count;
+    c->materials = (hk_material*)xdup(&sc->materials, sizeof(hk_material)); c->n_materials = sc->materials.count;
+    c->emissive_nodes = (hk_node*)xdup(&sc->emissive_nodes, sizeof(hk_node)); c->n_emissive_nodes = sc->emissive_nodes.count;
+    c->emissives = (hk_emissive*)xdup(&sc->emissives, sizeof(hk_emissive)); c->n_emissives = sc->emissives.count;
+    if (old_n != c->n_instances) { /* a different instance set: no history */
+        free(c->prev_models);
+        c->prev_models = (float*)calloc((size_t)(c->n_instances ? c->n_instances : 1) * 16, sizeof(float));
+        for (uint32_t i = 0; i < c->n_instances; ++i) memcpy(c->prev_models + 16 * (size_t)i, c->instances[i].model, 64);
     }
 }
 

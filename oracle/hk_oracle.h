@@ -40,6 +40,8 @@ void hko_sample_texture(const hko_ctx* ctx, uint32_t id, const float* uv, uint32
 /* restrict every pass to rows [y0 - halo, y0 + rows + halo) (multi-rank band tests; ratio 1) */
 void hko_set_band(hko_ctx* ctx, int32_t y0, int32_t rows, int32_t halo);
 
+/* replace the scene (e.g. after moving instances); the previous models of the motion vectors stay */
+void hko_set_scene(hko_ctx* ctx, const hk_scene_desc* scene);
 void hko_render_gbuffer(hko_ctx* ctx, const hk_frame_inputs* inputs);
 void hko_render_frame(hko_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs);
 void hko_denoise(hko_ctx* ctx, const hk_settings* settings, const hk_frame_inputs* inputs);

@@ -35,6 +35,7 @@ def lib() -> C.CDLL:
         "hko_destroy": (None, [vp]),
         "hko_set_band": (None, [vp, C.c_int32, C.c_int32, C.c_int32]),
         "hko_render_gbuffer": (None, [vp, vp]),
+        "hko_set_scene": (None, [vp, vp]),
         "hko_render_frame": (None, [vp, vp, vp]),
         "hko_denoise": (None, [vp, vp, vp]),
         "hko_tone_sum": (None, [vp, vp]),
@@ -107,6 +108,10 @@ class Oracle:
 
     def post_process(self, settings, inputs):
         self._L.hko_post_process(self.ctx, C.byref(settings), C.byref(inputs))
+
+    def set_scene(self, scene_desc):
+        """Replace the scene arrays (moved instances); the motion vectors' previous models stay."""
+        self._L.hko_set_scene(self.ctx, C.byref(scene_desc))
 
     def render_gbuffer(self, inputs):
         self._L.hko_render_gbuffer(self.ctx, C.byref(inputs))

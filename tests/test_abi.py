@@ -37,7 +37,7 @@ def test_abi_version_and_defaults():
 
     import hikari_amd
     L = hikari_amd._abi.lib()
-    assert L.hk_abi_version() == 1
+    assert L.hk_abi_version() == 2
     s = hikari_amd._abi.hk_settings()
     L.hk_settings_default(C.byref(s))
     # HikariSettings::default() (lib.rs:435-455)

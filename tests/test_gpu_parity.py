@@ -51,8 +51,10 @@ def lds_mode(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("size", [(64, 64), (96, 72)])
+@pytest.mark.parametrize("size", [(64, 64), (96, 72), (256, 256)])
 def test_cornell_frames_bit_exact(size, lds_mode):
+    """(256, 256): BASELINE configs[0] (examples/cornell.rs 256x256, all passes incl. spatial reuse
+    and the denoiser)."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     w, h = size
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
