@@ -12,9 +12,12 @@ denoiser read up to 36 rows away); each rank renders its rows, the tone-mapped R
 all-gathered over RCCL (stripes are then put back in frame order on a side stream), so every
 rank ends each step with the whole frame.  Total work is fixed => "strong" scaling.
 
-Mrays/s = traversal queries issued for the frame's own pixels (primary rays + every
-traverse_top + every emitter traverse_bottom of select_light_candidate; device counters,
-halo rows excluded) / wall time.
+Mrays/s = traversal queries of the light passes issued for the frame's own pixels
+(every traverse_top + every emitter traverse_bottom of select_light_candidate; device counters,
+halo rows excluded) / wall time.  This build's primary rays (the reference rasterises its G-buffer)
+are reported separately (`primary_mrays`), as is the primary-equivalent rate W*H*spp / t.
+`ms_per_step` is pipelined throughput (frame f's G-buffer overlaps frame f-1's light passes, its
+tail frame f+1's); `latency_ms` is one frame alone with frame pipelining off (median of 10).
 """
 from __future__ import annotations
 
@@ -35,7 +38,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
-from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
+from hikari_amd import HikariRenderer, HikariSettings, Taa, Upscale, examples, frame_inputs  # noqa: E402
 from hikari_amd.bands import band_of, halo_rows, stripe_gather_rows, use_stripes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -50,6 +53,7 @@ BYTES_PER_PIXEL = {
     "direct_lit_emissive": 368,      # both passes in one launch (k_direct_fused)
     "indirect_lit_ambient": 184,
     "indirect_multiple_bounces": 184,
+    "indirect_wavefront": 184,       # the same compulsory streams (queues / hit records are extra traffic)
     "indirect_spatial_reuse": 244,   # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8
     "emissive_spatial_reuse": 244,
     "demodulation": 92,              # 3 channels x (render 8 + variance 4 + internal 8 + ivar 4) + albedo 8 + G 12 + geom 32
@@ -80,9 +84,10 @@ CONFIGS = {
                                   workload="examples/cornell.rs 64x64 (host/launch overhead probe)"),
     # configs[4]: 16 integrator sub-frames (each one reference frame) accumulated per displayed frame,
     # one all-gather per displayed frame
-    "city-4k-16spp": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, spp=16,
+    "city-4k-16spp": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, spp=16, wavefront=True,
                           workload="examples/city.rs layout (City proxy houses) 3840x2160 16spp accumulation "
-                                   "(16 sub-frames per displayed frame), row bands + RCCL all-gather"),
+                                   "(16 sub-frames per displayed frame), wavefront material-sorted indirect "
+                                   "shading, row bands + RCCL all-gather"),
 }
 
 
@@ -101,7 +106,7 @@ def cpu_baseline(scene_desc, cam, lights, st, w, h, budget_s: float) -> dict:
     threads = cpu_threads()
     o = Oracle(scene_desc, hikari_amd.load_noise(), w, h, st.upscale.ratio(), threads=threads)
     s = st.to_c()
-    rays = 0
+    rays = primary = 0
     frames = 0
     t0 = time.perf_counter()
     while frames < 64:
@@ -113,14 +118,15 @@ def cpu_baseline(scene_desc, cam, lights, st, w, h, budget_s: float) -> dict:
             o.denoise(s, fi)
         o.tone_sum(s)
         c = o.counters()
-        rays += c["traverse_top"] + c["traverse_emitter"] + c["primary"]
+        rays += c["traverse_top"] + c["traverse_emitter"]
+        primary += c["primary"]
         frames += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     o.close()
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "ms_per_frame": round(dt / frames * 1e3, 1),
+            "ms_per_frame": round(dt / frames * 1e3, 1), "primary_mrays": round(primary / dt / 1e6, 3),
             "sample": f"same workload, frames 0..{frames - 1} ({frames} frames, {dt:.1f} s) on the CPU oracle "
                       f"(C restatement of light.wgsl/denoise.wgsl, {threads} OpenMP threads)"}
 
@@ -147,6 +153,20 @@ def load_traversal_bytes(config: str):
         return None
     try:
         return json.loads(p.read_text())["configs"][config]["traversal_bytes_per_frame"]
+    except (KeyError, ValueError):
+        return None
+
+
+def load_lane_efficiency(config: str, wavefront: bool):
+    """traverse_top SIMD lane efficiency per kernel (active lanes / (64 x walk iterations)) of `config`
+    from the committed instrumented-build measurement (profiles/r02/lane_stats.json, tools/lane_stats.py);
+    the 16-spp config's sub-frames are city-4k frames."""
+    p = ROOT / "profiles" / "r02" / "lane_stats.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())["configs"][{"city-4k-16spp": "city-4k"}.get(config, config)]
+        return {k: v["efficiency"] for k, v in d["wavefront" if wavefront else "megakernel"].items()}
     except (KeyError, ValueError):
         return None
 
@@ -181,7 +201,9 @@ def main():
     W, H = cfg["width"], cfg["height"]
     scene, cam, lights = examples.SCENES[cfg["scene"]]()
     desc = scene.build()
-    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
+    # SURVEY §8d common settings: SMAA TU4x at ratio 1.0 (s = S), taa None (no prepass jitter)
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, taa=Taa.None_, indirect_spatial_reuse=cfg["spatial"],
+                        denoise=cfg["denoise"])
     s = st.to_c()
 
     # rows of this rank (hikari_amd/bands.py): interleaved stripes, or a contiguous band + halo
@@ -190,6 +212,10 @@ def main():
     r.set_noise()
     r.upload_scene(scene)
     r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
+    # the indirect pass as a wavefront with material-sorted shading (hk_set_wavefront); HK_BENCH_WAVEFRONT
+    # overrides the config (0 = megakernel, 1 = wavefront) for comparisons
+    wavefront = os.environ.get("HK_BENCH_WAVEFRONT", "1" if cfg.get("wavefront") else "0") == "1"
+    r.set_wavefront(wavefront)
     if stripes:
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
@@ -300,14 +326,38 @@ def main():
     elapsed = time.perf_counter() - t0
     timing = r.kernel_timing()
     c = r.counters()
-    rays = c["traverse_top"] + c["traverse_emitter"] + c["primary"]
+    rays = c["traverse_top"] + c["traverse_emitter"]
+    primary = c["primary"]
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-        n = torch.tensor([rays], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
+        n = torch.tensor([rays, primary], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        rays = int(n.item())
+        rays, primary = int(n[0].item()), int(n[1].item())
+
+    # per-frame latency: frames alone (frame pipelining off), each bracketed by a device sync
+    latency = None
+    if world == 1 and not dynamic:
+        lat_env = {"HK_GB_PIPELINE": "0", "HK_DN_PIPELINE": "0"}
+        saved = {k: os.environ.get(k) for k in lat_env}
+        os.environ.update(lat_env)
+        r.enable_kernel_timing(False)
+        f0 = args.warmup + args.steps
+        times = []
+        for f in range(f0, f0 + 10):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            step(f)
+            r.sync(sp)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t1)
+        latency = float(np.median(times)) * 1e3
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
     # after the timed region: a few frames with every kernel alone on the GPU (no channel fork, no
     # frame pipelining), so the roofline can also quote the dominant kernel's isolated duration
@@ -318,7 +368,7 @@ def main():
         os.environ.update(iso_env)
         r.set_kernel_timing_interval(1)
         r.enable_kernel_timing(True)
-        f0 = args.warmup + args.steps
+        f0 = args.warmup + args.steps + 10
         for f in range(f0, f0 + 8):
             step(f)
         torch.cuda.synchronize()
@@ -358,8 +408,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (static camera; reference assets: cornell.glb, blue noise)",
+            "latency_ms": None if latency is None else round(latency, 4),
+            "primary_mrays": round(primary / elapsed / 1e6, 2),
+            "primary_equivalent_mrays": round(W * H * spp * args.steps / elapsed / 1e6, 2),
             "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": spp,
-                       "rays_per_frame": int(rays // args.steps),
+                       "indirect": "wavefront material-sorted" if wavefront else "megakernel",
+                       "rays_per_frame": int(rays // (args.steps * spp)),
+                       "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
                                        f"row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -384,6 +439,9 @@ def main():
             # (L1/L2/MALL traffic: the scene is cache resident), over the frame time
             result["roofline"]["frame_traversal_bytes"] = tb
             result["roofline"]["frame_traversal_achieved"] = round(tb / (ms * 1e-3) / 1e9, 1)
+        lanes = load_lane_efficiency(args.config, wavefront)
+        if lanes is not None:
+            result["roofline"]["lane_efficiency"] = lanes
         if world == 1 and args.cpu_budget > 0:
             result["cpu_baseline"] = cpu_baseline(desc, cam, lights, st, W, H, args.cpu_budget)
         else:

@@ -799,6 +799,37 @@ HKD f3 local_to_world_normal(const hk_instance& in, f3 n)
 // lanes wait.  Here all lanes share every iteration's node load and slab test; only the leaf
 // work (instance entry, triangle test) diverges.  Cornell 1080p: direct 0.185 -> 0.168 ms,
 // indirect 0.311 -> 0.286 ms; scene 1080p emissive 0.476 -> 0.421 ms.
+// Lane-efficiency instrumentation (experiment builds only, EXTRA=-DHK_LANE_STATS): every iteration
+// of a traverse_top walk adds the wave's active lanes (its first active lane counts for the wave), so
+// sum(active) / (64 x sum(iterations)) is the fraction of SIMD lanes doing walk work, idle lanes of
+// the wave (walks already ended, lanes with no ray) included.
+#ifdef HK_LANE_STATS
+extern __device__ unsigned long long hk_lane_stats_dev[2];
+struct LaneStats {
+    unsigned long long act = 0, its = 0;
+    HKD void tick()
+    {
+        const unsigned long long m = __ballot(1);
+        if ((uint32_t)__builtin_ctzll(m) == (threadIdx.x & 63u)) {
+            act += (unsigned long long)__builtin_popcountll(m);
+            its += 1;
+        }
+    }
+    HKD ~LaneStats()
+    {
+        if (its) {
+            atomicAdd(&hk_lane_stats_dev[0], act);
+            atomicAdd(&hk_lane_stats_dev[1], its);
+        }
+    }
+};
+#define HK_LANE_STATS_DECL LaneStats lane_stats_
+#define HK_LANE_STATS_TICK lane_stats_.tick()
+#else
+#define HK_LANE_STATS_DECL
+#define HK_LANE_STATS_TICK
+#endif
+
 #if HK_TRAVERSE_PAIRSTEP
 // Several visits per iteration where the order allows it (walk_step): an inner child-box node p
 // that passes is always followed by node p + 1 (its subtree start, bvh flatten), tested with the
@@ -818,8 +849,10 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
     uint32_t bot_base = 0u, prim_offset = 0u, cur_instance = 0u;
     bool in_bottom = false, intersected = false;
     Ray local = ray;
+    HK_LANE_STATS_DECL;
     for (;;) {
         if (!in_bottom && top >= sc.n_instance_nodes) break;
+        HK_LANE_STATS_TICK;
         const hk_node* nodes = in_bottom ? sc.asset_nodes + bot_base : sc.instance_nodes;
         const uint32_t count = in_bottom ? bot_count : sc.n_instance_nodes;
         const uint32_t index = in_bottom ? bot : top;
@@ -889,8 +922,10 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
     uint32_t bot_base = 0u, prim_offset = 0u, cur_instance = 0u;
     bool in_bottom = false, intersected = false;
     Ray local = ray;
+    HK_LANE_STATS_DECL;
     for (;;) {
         if (!in_bottom && top >= sc.n_instance_nodes) break;
+        HK_LANE_STATS_TICK;
         const hk_node* nodes = in_bottom ? sc.asset_nodes + bot_base : sc.instance_nodes;
         const uint32_t index = in_bottom ? bot : top;
         f3 mn, mx;

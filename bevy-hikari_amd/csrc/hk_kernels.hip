@@ -20,6 +20,24 @@
 
 namespace hk {
 
+#ifdef HK_LANE_STATS
+__device__ unsigned long long hk_lane_stats_dev[2];
+#endif
+// traverse_top lane statistics since the last call (instrumented builds; false otherwise)
+bool lane_stats_take(unsigned long long out[2], hipStream_t st)
+{
+#ifdef HK_LANE_STATS
+    unsigned long long zero[2] = {0, 0};
+    if (hipStreamSynchronize(st) != hipSuccess) return false;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hk_lane_stats_dev), sizeof(zero)) != hipSuccess) return false;
+    return hipMemcpyToSymbol(HIP_SYMBOL(hk_lane_stats_dev), zero, sizeof(zero)) == hipSuccess;
+#else
+    (void)st;
+    out[0] = out[1] = 0;
+    return false;
+#endif
+}
+
 // workgroup -> 16x16 tile -> pixel (global coordinates).  Tile orders:
 // RASTER: blockIdx in raster order; workgroups are dealt round-robin over the 8 XCDs, so every
 //   XCD works on the same band of the frame at once and per-region cost differences (sky vs.
@@ -437,9 +455,33 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
 }
 
 // ------------------------------------------------------------------ indirect_lit_ambient (light.wgsl:1263-1498)
-template <bool MULTI>
-HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top, uint32_t& n_emitter)
+// The pass runs either as one megakernel (IND_ALL: one thread per pixel, start to end) or as the
+// wavefront pipeline of config 5 (WfArgs below): IND_GEN (the dead-pixel stores; live pixels go to a
+// compacted queue), IND_TRACE (the cosine bounce's closest hit, stored as an SoA hit record, keyed
+// by the hit's material), IND_SHADE (in material order: the rest of the pass from the stored hit).
+// The stages run the same statements in the same order for a pixel, so results are identical.
+enum IndStage : int { IND_ALL = 0, IND_GEN = 1, IND_TRACE = 2, IND_SHADE = 3 };
+HKD void wf_store_hit(const WfArgs& W, int32_t idx, const Hit& h)
 {
+    W.hit[idx] = make_uint4(h.instance_index, h.primitive_index, __float_as_uint(h.uv.x), __float_as_uint(h.uv.y));
+    W.hit_t[idx] = h.distance;
+}
+HKD Hit wf_load_hit(const WfArgs& W, int32_t idx)
+{
+    const uint4 v = W.hit[idx];
+    Hit h;
+    h.instance_index = v.x;
+    h.primitive_index = v.y;
+    h.uv = mk2(__uint_as_float(v.z), __uint_as_float(v.w));
+    h.distance = W.hit_t[idx];
+    return h;
+}
+// returns (IND_GEN) whether the pixel traces a bounce; (IND_TRACE) the hit's material bin in *key
+template <bool MULTI, int STAGE = IND_ALL>
+HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
+                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr)
+{
+    static_assert(!MULTI || STAGE == IND_ALL, "the wavefront stages cover one bounce");
     const Frame& F = A.F;
     const int32_t idx = s_index(F, x, y);
     const f2 uv = coords_to_uv(x, y, F.s);
@@ -451,13 +493,16 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
     Sample s = zero_sample();
     Reservoir r = zero_reservoir();
     if (F.indirect_bounces == 0u || depth < HK_F32_EPSILON) {
-        store_res(C.cur, idx, r);
-        store_res(C.spatial, idx, r);
-        store_res(C.prev_spatial, idx, r);
-        C.variance[idx] = 0.0f;
-        store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
-        return;
+        if constexpr (STAGE == IND_ALL || STAGE == IND_GEN) {
+            store_res(C.cur, idx, r);
+            store_res(C.spatial, idx, r);
+            store_res(C.prev_spatial, idx, r);
+            C.variance[idx] = 0.0f;
+            store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
+        }
+        return false;
     }
+    if constexpr (STAGE == IND_GEN) return true;
     f3 normal = normalize(load_normal(F, A.G, dx, dy));
     f2 imf = load_instance_material(F, A.G, dx, dy);
     uint32_t im_x = f2u32(imf.x), im_y = f2u32(imf.y);
@@ -537,8 +582,18 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
         normal_basis(s.visible_normal, bt, bb);
         ray.direction = basis_mul(bt, bb, s.visible_normal, xyz(rs));
         ray.inv_direction = inv(ray.direction);
-        n_top++;
-        Hit hit = traverse_top(sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+        Hit hit;
+        if constexpr (STAGE == IND_SHADE) {
+            hit = wf_load_hit(*W, idx);
+        } else {
+            n_top++;
+            hit = traverse_top(sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+        }
+        if constexpr (STAGE == IND_TRACE) {
+            wf_store_hit(*W, idx, hit);
+            *key = hit.instance_index != HK_U32_MAX ? min(get_instance(sc, hit.instance_index).material, W->bins - 2u) : W->bins - 1u;
+            return true;
+        }
         info = hit_info(sc, ray, hit);
         s.sample_position = info.position;
         s.sample_normal = info.normal;
@@ -593,6 +648,7 @@ HKD void indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
     if (F.temporal_reuse > 0u) store_res(C.cur, idx, r);
     f3 o = out * r.w;
     store_rgba16f(C.render, idx, mk4(o.x, o.y, o.z, 1.0f));
+    return true;
 }
 
 template <bool MULTI, bool LDS>
@@ -605,6 +661,168 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
+// ------------------------------------------------------------------ wavefront indirect pass (config 5)
+// BASELINE configs[4] asks for wavefront, material-sorted shading.  The megakernel k_indirect runs
+// one thread per pixel from the G-buffer to the stored reservoir; lanes of sky pixels idle through
+// the bounce walk and a wave's lanes hit unrelated materials.  Here the pass is five launches:
+//   k_wf_gen      per 16x16 tile: dead pixels (sky, bounces 0) do their stores; live pixels are
+//                 compacted into queue1 (wave64 ballot + prefix popcount inside the workgroup, one
+//                 atomic per workgroup on its segment's counter)
+//   k_wf_trace    per 256 queue1 entries: the cosine bounce's closest hit (traverse_top), written
+//                 as an SoA hit record; the hit's material bin goes to keys[] and the segment's
+//                 histogram (one atomic per wave and distinct bin)
+//   k_wf_scan     one workgroup: bin totals, their exclusive prefix sum, each segment's offset in
+//                 each bin -> bin write cursors
+//   k_wf_scatter  per 256 queue1 entries: pixels into queue2 grouped by bin (per wave and bin one
+//                 atomic on the segment's cursor, ranks from the ballot)
+//   k_wf_shade    per 256 queue2 entries, in bin order: hit_info, surface fetch, NEE (light-BVH pick,
+//                 emitter BLAS walk, shadow any-hit) and the temporal ReSTIR tail
+// A pixel executes the statements of indirect_body in the same order (the stages stop / resume at
+// the bounce hit), so every stored word equals the megakernel's.  Grids are sized for the largest
+// queue; workgroups past the live count exit at once.  Atomics on one shared word (a queue cursor
+// or the hottest bin) serialise at the L2, so every counter is split over WF_SEGS segments.
+HKD uint32_t wave_rank(uint64_t m) { return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)); }
+HKD uint32_t wf_pack(int32_t x, int32_t ly) { return (uint32_t)x | ((uint32_t)ly << 16); }
+HKD void wf_unpack(const Frame& F, uint32_t p, int32_t& x, int32_t& y)
+{
+    x = (int32_t)(p & 0xFFFFu);
+    y = global_row(F, (int32_t)(p >> 16), F.s_row0);
+}
+// per wave: for each distinct key among the active lanes, one atomicAdd of its lane count on
+// base[key]; returns the lane's slot (base + rank among the lanes with its key)
+HKD uint32_t wf_bin_slot(uint32_t* base, bool active, uint32_t key)
+{
+    uint64_t left = __ballot(active);
+    uint32_t slot = 0;
+    while (left) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(left);
+        const uint32_t k = __shfl(key, (int)leader, 64);
+        const uint64_t same = __ballot(active && key == k);
+        uint32_t b = 0;
+        if ((threadIdx.x & 63u) == leader) b = atomicAdd(base + k, (uint32_t)__builtin_popcountll(same));
+        b = __shfl(b, (int)leader, 64);
+        if (active && key == k) slot = b + wave_rank(same);
+        left &= ~same;
+    }
+    return slot;
+}
+// the queue1 entry of this thread for the per-entry kernels: workgroup b -> segment b % WF_SEGS,
+// entries 256 (b / WF_SEGS) .. of that segment; false past the segment's live count
+HKD bool wf_entry(const WfArgs& W, uint32_t& seg, uint32_t& i)
+{
+    seg = blockIdx.x % WF_SEGS;
+    i = (blockIdx.x / WF_SEGS) * 256u + threadIdx.x;
+    return i < W.ctl[seg];
+}
+
+__global__ __launch_bounds__(256) void k_wf_gen(FrameArgs A, ChannelArgs C, WfArgs W)
+{
+    __shared__ uint32_t wave_n[4], wg_base;
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    bool live = false;
+    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+        live = indirect_body<false, IND_GEN>(A, A.sc, C, x, y, n_top, n_emitter);
+    const uint64_t m = __ballot(live);
+    const uint32_t wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0u) wave_n[wave] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    // tiles dealt round-robin over the segments: the workgroups in flight (neighbouring tiles) append
+    // to different counters (contiguous runs of tiles per segment measured slower: city 4K 16 spp
+    // 121.1 -> 124.9 ms, the concurrent workgroups then share one counter); a segment's entries
+    // stay grouped by tile, so a wave of a bin still holds one tile's pixels
+    const uint32_t tile = blockIdx.x + blockIdx.y * gridDim.x, seg = tile % WF_SEGS;
+    if (threadIdx.x == 0) {
+        const uint32_t total = wave_n[0] + wave_n[1] + wave_n[2] + wave_n[3];
+        wg_base = total ? atomicAdd(&W.ctl[seg], total) : 0u;
+    }
+    __syncthreads();
+    uint32_t off = wg_base;
+    for (uint32_t k = 0; k < wave; ++k) off += wave_n[k];
+    if (live) W.queue1[seg * W.seg_cap + off + wave_rank(m)] = wf_pack(x, local_row(A.F, y, A.F.s_row0));
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_wf_trace(FrameArgs A, ChannelArgs C, WfArgs W)
+{
+    uint32_t seg, i;
+    const bool valid = wf_entry(W, seg, i);
+    if ((blockIdx.x / WF_SEGS) * 256u >= W.ctl[seg]) return;  // the whole workgroup is past the count
+    Scene sc;
+    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+    else sc = A.sc;
+    uint32_t n_top = 0, n_emitter = 0, key = 0;
+    if (valid) {
+        int32_t x, y;
+        wf_unpack(A.F, W.queue1[seg * W.seg_cap + i], x, y);
+        indirect_body<false, IND_TRACE>(A, sc, C, x, y, n_top, n_emitter, &W, &key);
+        if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = 0;
+        W.keys[seg * W.seg_cap + i] = key;
+    }
+    (void)wf_bin_slot(W.ctl + WF_CTL_HIST + seg * W.bins, valid, key);  // the segment's histogram
+    wave_count(A.cnt.top, n_top);
+}
+
+__global__ __launch_bounds__(256) void k_wf_scan(WfArgs W)
+{
+    __shared__ uint32_t part[256];
+    const uint32_t bins = W.bins, t = threadIdx.x;
+    const uint32_t per = (bins + 255u) / 256u, b0 = t * per, b1 = min(bins, b0 + per);
+    const uint32_t* hist = W.ctl + WF_CTL_HIST;
+    uint32_t* cursor = W.ctl + WF_CTL_HIST + WF_SEGS * bins;
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b)
+        for (uint32_t g = 0; g < WF_SEGS; ++g) sum += hist[g * bins + b];
+    part[t] = sum;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < 256u; ++k) {
+            const uint32_t v = part[k];
+            part[k] = acc;
+            acc += v;
+        }
+        W.ctl[WF_SEGS] = acc;  // all live pixels
+    }
+    __syncthreads();
+    uint32_t acc = part[t];
+    for (uint32_t b = b0; b < b1; ++b)
+        for (uint32_t g = 0; g < WF_SEGS; ++g) {
+            cursor[g * bins + b] = acc;
+            acc += hist[g * bins + b];
+        }
+}
+
+__global__ __launch_bounds__(256) void k_wf_scatter(WfArgs W)
+{
+    uint32_t seg, i;
+    const bool valid = wf_entry(W, seg, i);
+    if ((blockIdx.x / WF_SEGS) * 256u >= W.ctl[seg]) return;
+    const uint32_t key = valid ? W.keys[seg * W.seg_cap + i] : 0u;
+    const uint32_t slot = wf_bin_slot(W.ctl + WF_CTL_HIST + WF_SEGS * W.bins + seg * W.bins, valid, key);
+    if (valid) W.queue2[slot] = W.queue1[seg * W.seg_cap + i];
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_wf_shade(FrameArgs A, ChannelArgs C, WfArgs W)
+{
+    const uint32_t n = W.ctl[WF_SEGS];
+    if (blockIdx.x * 256u >= n) return;
+    Scene sc;
+    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+    else sc = A.sc;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    uint32_t n_top = 0, n_emitter = 0;
+    if (i < n) {
+        int32_t x, y;
+        wf_unpack(A.F, W.queue2[i], x, y);
+        indirect_body<false, IND_SHADE>(A, sc, C, x, y, n_top, n_emitter, &W);
+        if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    }
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -1036,6 +1254,20 @@ void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipSt
         if (lds) hipLaunchKernelGGL((k_indirect<false, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_indirect<false, false>), g, dim3(256), 0, st, A, C);
     }
+}
+void launch_indirect_wavefront(const FrameArgs& A, const ChannelArgs& C, const WfArgs& W, hipStream_t st)
+{
+    const dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, true);
+    const dim3 per_seg(WF_SEGS * (W.seg_cap / 256u));      // every segment's entries, 256 per workgroup
+    const dim3 all(((uint32_t)A.F.s[0] * (uint32_t)A.F.s_rows + 255u) / 256u);
+    hipLaunchKernelGGL(k_wf_gen, g, dim3(256), 0, st, A, C, W);
+    if (lds) hipLaunchKernelGGL(k_wf_trace<true>, per_seg, dim3(256), lds, st, A, C, W);
+    else hipLaunchKernelGGL(k_wf_trace<false>, per_seg, dim3(256), 0, st, A, C, W);
+    hipLaunchKernelGGL(k_wf_scan, dim3(1), dim3(256), 0, st, W);
+    hipLaunchKernelGGL(k_wf_scatter, per_seg, dim3(256), 0, st, W);
+    if (lds) hipLaunchKernelGGL(k_wf_shade<true>, all, dim3(256), lds, st, A, C, W);
+    else hipLaunchKernelGGL(k_wf_shade<false>, all, dim3(256), 0, st, A, C, W);
 }
 void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
 {

@@ -28,6 +28,27 @@ struct ChannelArgs {
     uint2* render;
 };
 
+// Wavefront indirect pass (config 5: material-sorted shading), see hk_kernels.hip k_wf_*.
+// The live-pixel queue is split into WF_SEGS segments (tile t -> segment t % WF_SEGS, each with room
+// for all its tiles' pixels) so that appends and the material histogram spread their atomics over
+// WF_SEGS addresses.  ctl words: [s] live pixels of segment s, [WF_SEGS] all live pixels,
+// [WF_CTL_HIST + s * bins + b] segment s's pixels in material bin b, then the same layout of bin
+// write cursors.
+constexpr uint32_t WF_SEGS = 64;
+constexpr uint32_t WF_CTL_HIST = WF_SEGS + 16;
+constexpr uint32_t WF_MAX_BINS = 4096;  // materials + 1 (misses); larger scenes use the megakernel
+struct WfArgs {
+    uint32_t* queue1;  // live pixels (x | local row << 16): segment s at [s * seg_cap, s * seg_cap + count)
+    uint32_t* keys;    // material bin per queue1 slot
+    uint32_t* queue2;  // all live pixels, grouped by material bin
+    uint4* hit;        // per pixel (s plane): instance, primitive, u bits, v bits of the bounce hit
+    float* hit_t;      // per pixel: its distance
+    uint32_t* ctl;
+    uint32_t bins;     // n_materials + 1
+    uint32_t seg_cap;  // queue1 slots per segment: 256 x ceil(tiles / WF_SEGS)
+};
+constexpr uint32_t wf_ctl_words(uint32_t bins) { return WF_CTL_HIST + 2u * WF_SEGS * bins; }
+
 struct ViewArgs {
     float world_position[3];
     float view_proj[16];
@@ -94,11 +115,15 @@ void launch_smaa(const PostArgs& P, hipStream_t st);
 void launch_smaa_extrapolate(const PostArgs& P, hipStream_t st);
 void launch_taa(const PostArgs& P, hipStream_t st);
 
+bool lane_stats_take(unsigned long long out[2], hipStream_t st);
 void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32_t stack_need, hipStream_t st);
 void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, hipStream_t st);
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st);
 void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st);
+// the wavefront indirect pass (one bounce): gen + compaction, bounce trace, bin scan, scatter by
+// material, material-sorted shade; W.ctl must be zeroed on `st` before
+void launch_indirect_wavefront(const FrameArgs& A, const ChannelArgs& C, const WfArgs& W, hipStream_t st);
 void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st);
 void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st);

@@ -136,6 +136,15 @@ struct hk_ctx {
     uint32_t accum_n = 0;
     // counters (top, emitter, primary)
     unsigned long long* counters = nullptr;
+    // wavefront indirect pass (hk_set_wavefront): queues, SoA hit records, control words
+    bool wavefront = false;
+    uint32_t* wf_queue1 = nullptr;
+    uint32_t* wf_keys = nullptr;
+    uint32_t* wf_queue2 = nullptr;
+    uint4* wf_hit = nullptr;
+    float* wf_hit_t = nullptr;
+    uint32_t* wf_ctl = nullptr;
+    uint32_t wf_seg_cap = 0;
 
     // timing
     bool timing = false;
@@ -146,6 +155,9 @@ struct hk_ctx {
     std::vector<std::string> timing_names;
     std::vector<double> timing_ms;
     std::vector<uint64_t> timing_n;
+    // traverse_top lane statistics per timed launch name (instrumented builds, hk_lane_stats)
+    std::vector<std::string> lane_names;
+    std::vector<unsigned long long> lane_act, lane_its;
 };
 
 namespace {
@@ -280,7 +292,29 @@ void free_targets(hk_ctx* c)
     release(c->accum);
     release(c->accum_out);
     c->accum_n = 0;
+    release(c->wf_queue1);
+    release(c->wf_keys);
+    release(c->wf_queue2);
+    release(c->wf_hit);
+    release(c->wf_hit_t);
+    release(c->wf_ctl);
     c->sized = false;
+}
+
+// the wavefront pass's buffers, allocated on first use after a resize (s-plane sized)
+int ensure_wavefront(hk_ctx* c)
+{
+    if (c->wf_ctl) return HK_OK;
+    const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
+    const size_t tiles = (size_t)((c->s[0] + 15u) / 16u) * (size_t)(((uint32_t)c->s_rows + 15u) / 16u);
+    c->wf_seg_cap = (uint32_t)(256u * ((tiles + WF_SEGS - 1u) / WF_SEGS));
+    HK_HIP(c, hipMalloc(&c->wf_queue1, (size_t)WF_SEGS * c->wf_seg_cap * 4));
+    HK_HIP(c, hipMalloc(&c->wf_keys, (size_t)WF_SEGS * c->wf_seg_cap * 4));
+    HK_HIP(c, hipMalloc(&c->wf_queue2, n * 4));
+    HK_HIP(c, hipMalloc(&c->wf_hit, n * sizeof(uint4)));
+    HK_HIP(c, hipMalloc(&c->wf_hit_t, n * 4));
+    HK_HIP(c, hipMalloc(&c->wf_ctl, (size_t)wf_ctl_words(WF_MAX_BINS) * 4));
+    return HK_OK;
 }
 
 hipEvent_t take_event(hk_ctx* c)
@@ -296,9 +330,34 @@ hipEvent_t take_event(hk_ctx* c)
 }
 
 // Launch wrapper: records HIP events around the kernel on its own stream when timing is on.
+void lane_stats_account(hk_ctx* c, const char* name, hipStream_t st)
+{
+    unsigned long long v[2];
+    if (!lane_stats_take(v, st) || !v[1]) return;
+    size_t k = 0;
+    for (; k < c->lane_names.size(); ++k)
+        if (c->lane_names[k] == name) break;
+    if (k == c->lane_names.size()) {
+        c->lane_names.push_back(name);
+        c->lane_act.push_back(0);
+        c->lane_its.push_back(0);
+    }
+    c->lane_act[k] += v[0];
+    c->lane_its[k] += v[1];
+}
+
 template <typename F>
 void timed(hk_ctx* c, const char* name, hipStream_t st, F&& launch)
 {
+#ifdef HK_LANE_STATS
+    // instrumented build: attribute the walk statistics to this launch (serialises the streams)
+    (void)hipDeviceSynchronize();
+    unsigned long long drop[2];
+    (void)lane_stats_take(drop, st);
+    launch();
+    lane_stats_account(c, name, st);
+    return;
+#endif
     if (!c->timing || !c->timing_frame) {
         launch();
         return;
@@ -1169,7 +1228,17 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(A, C1, true, s1); });
     ChannelArgs C2 = channel(c, A.F.number, 2);
     bool multi = settings->indirect_bounces >= 2u;
-    timed(c, multi ? "indirect_multiple_bounces" : "indirect_lit_ambient", s2, [&] { launch_indirect(A, C2, multi, s2); });
+    // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
+    const bool wf = c->wavefront && !multi && c->count[6] + 1u <= WF_MAX_BINS;
+    if (wf) {
+        HK_TRY(ensure_wavefront(c));
+        WfArgs W{c->wf_queue1, c->wf_keys, c->wf_queue2, c->wf_hit, c->wf_hit_t, c->wf_ctl, c->count[6] + 1u,
+                 c->wf_seg_cap};
+        HK_HIP(c, hipMemsetAsync(W.ctl, 0, (size_t)wf_ctl_words(W.bins) * 4, s2));
+        timed(c, "indirect_wavefront", s2, [&] { launch_indirect_wavefront(A, C2, W, s2); });
+    } else {
+        timed(c, multi ? "indirect_multiple_bounces" : "indirect_lit_ambient", s2, [&] { launch_indirect(A, C2, multi, s2); });
+    }
     if (settings->indirect_spatial_reuse) timed(c, "indirect_spatial_reuse", s2, [&] { launch_spatial(A, C2, false, s2); });
     if (fork) {
         HK_HIP(c, hipEventRecord(c->ev_join[1], s2));
@@ -1384,6 +1453,26 @@ const void* hk_output_device_ptr(hk_ctx* c, int id)
 {
     if (!c || !c->sized) return nullptr;
     return output_ptr(c, id, nullptr, nullptr, nullptr);
+}
+
+int hk_lane_stats(hk_ctx* c, const char** names, unsigned long long* active, unsigned long long* iterations,
+                  int capacity)
+{
+    if (!c) return HK_ERR_INVALID;
+    const int n = (int)c->lane_names.size();
+    for (int i = 0; i < n && i < capacity; ++i) {
+        if (names) names[i] = c->lane_names[i].c_str();
+        if (active) active[i] = c->lane_act[i];
+        if (iterations) iterations[i] = c->lane_its[i];
+    }
+    return n;
+}
+
+int hk_set_wavefront(hk_ctx* c, int enable)
+{
+    if (!c) return HK_ERR_INVALID;
+    c->wavefront = enable != 0;
+    return HK_OK;
 }
 
 int hk_sync(hk_ctx* c, void* stream)

@@ -159,6 +159,8 @@ def lib() -> C.CDLL:
         "hk_get_output": (i32, [vp, i32, vp, C.c_size_t, i32, vp]),
         "hk_output_device_ptr": (vp, [vp, i32]),
         "hk_sync": (i32, [vp, vp]),
+        "hk_set_wavefront": (i32, [vp, i32]),
+        "hk_lane_stats": (i32, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), i32]),
         "hk_dump_reservoirs": (i32, [vp, i32, vp, C.c_size_t, vp]),
         "hk_load_reservoirs": (i32, [vp, i32, vp, C.c_size_t, vp]),
         "hk_reset_counters": (i32, [vp, vp]),
@@ -191,7 +193,7 @@ def lib() -> C.CDLL:
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
     "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
-    "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_sync", "hk_dump_reservoirs",
+    "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_sync", "hk_set_wavefront", "hk_lane_stats", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing", "hk_set_kernel_timing_interval",
     "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hk_selftest_rcp", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",
     "hks_add_instance", "hks_build", "hks_get_desc",

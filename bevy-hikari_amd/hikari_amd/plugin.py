@@ -148,6 +148,10 @@ class HikariRenderer:
         """Device address of the plane for this frame (call sync(stream) before reading it there)."""
         return self._L.hk_output_device_ptr(self.ctx, output_id)
 
+    def set_wavefront(self, enable: bool = True) -> None:
+        """Indirect pass as a wavefront with material-sorted shading (hk_set_wavefront)."""
+        _check(self.ctx, self._L.hk_set_wavefront(self.ctx, int(enable)), "hk_set_wavefront")
+
     def sync(self, stream=None) -> None:
         """`stream` waits for the context's own streams (hk_sync)."""
         _check(self.ctx, self._L.hk_sync(self.ctx, stream), "hk_sync")
@@ -185,6 +189,14 @@ class HikariRenderer:
     def set_kernel_timing_interval(self, every: int) -> None:
         """Time only frames whose frame_number % every == 0 (hk_set_kernel_timing_interval)."""
         _check(self.ctx, self._L.hk_set_kernel_timing_interval(self.ctx, int(every)), "hk_set_kernel_timing_interval")
+
+    def lane_stats(self) -> dict:
+        """{kernel: (active lanes, walk iterations)} of traverse_top (instrumented builds only)."""
+        names = (C.c_char_p * 64)()
+        act = (C.c_uint64 * 64)()
+        its = (C.c_uint64 * 64)()
+        n = self._L.hk_lane_stats(self.ctx, names, act, its, 64)
+        return {names[i].decode(): (int(act[i]), int(its[i])) for i in range(min(n, 64))}
 
     def kernel_timing(self) -> dict:
         names = (C.c_char_p * 64)()

@@ -285,6 +285,11 @@ int hk_get_output(hk_ctx* ctx, int output_id, void* dst, size_t bytes, int to_ho
 const void* hk_output_device_ptr(hk_ctx* ctx, int output_id);
 /* Make `stream` wait (device-side) for all work the context queued on its own streams. */
 int hk_sync(hk_ctx* ctx, void* stream);
+/* Integrator layout of the indirect pass (light.wgsl:1263-1498, one bounce): 0 = one thread per
+ * pixel (default); 1 = wavefront with material-sorted shading (BASELINE configs[4]): live pixels
+ * compacted into a queue, the bounce walk writes SoA hit records, the queue is grouped by the hit's
+ * material and the shading / NEE / shadow / temporal tail runs in that order.  Same results. */
+int hk_set_wavefront(hk_ctx* ctx, int enable);
 /* copy band-local rows [row0, row0+rows) of an output plane (e.g. the band's core rows for the
  * multi-GPU all-gather); dst is host (to_host=1) or device memory */
 int hk_copy_output_rows(hk_ctx* ctx, int output_id, uint32_t row0, uint32_t rows, void* dst, int to_host,
@@ -297,6 +302,11 @@ int hk_read_counters(hk_ctx* ctx, hk_counters* out, void* stream);
 /* mean duration (ms) of each kernel of the last hk_render_frame/hk_denoise call, if timing is enabled */
 int hk_enable_kernel_timing(hk_ctx* ctx, int enable);
 int hk_kernel_timing(hk_ctx* ctx, const char** names, float* ms, int capacity);
+/* traverse_top lane statistics per kernel name since hk_create, in builds compiled with
+ * -DHK_LANE_STATS (experiments; the product build returns 0 entries): per walk iteration the wave's
+ * active lanes, so active / (64 x iterations) is the walk's SIMD lane efficiency */
+int hk_lane_stats(hk_ctx* ctx, const char** names, unsigned long long* active, unsigned long long* iterations,
+                  int capacity);
 /* time only frames whose frame_number % every == 0 (default 1: every frame), so the timing
  * events of a long measured run do not perturb most of its frames */
 int hk_set_kernel_timing_interval(hk_ctx* ctx, uint32_t every);

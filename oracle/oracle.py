@@ -68,6 +68,18 @@ def lib() -> C.CDLL:
     return L
 
 
+def default_threads() -> int:
+    """OpenMP threads: OMP_NUM_THREADS if set (the GPU box sets it to the job's core share), else
+    the cores this process may run on (os.cpu_count() counts the whole machine there)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 class Oracle:
     """CPU restatement of one camera's integrator state (same API shape as HikariRenderer)."""
 
@@ -77,7 +89,7 @@ class Oracle:
         self._L = L
         self._noise = np.ascontiguousarray(noise, np.uint8)
         self.ctx = L.hko_create(C.byref(scene_desc), self._noise.ctypes.data, width, height, ratio,
-                                threads or (os.cpu_count() or 1))
+                                threads or default_threads())
         self.width, self.height = width, height
         if textures:
             self.set_textures(textures)
