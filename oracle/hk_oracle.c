@@ -161,6 +161,7 @@ struct hko_ctx {
     uint16_t* taa_buf[2]; uint32_t taa_wh[2];
     hk_counters counters;
     int32_t band_y0, band_y1; /* rows computed by every pass (whole frame by default) */
+    int32_t stripe_n, stripe_k; /* hko_set_stripes: only rows of 8-row stripes k, k + n, ... (n >= 2) */
 };
 
 typedef struct {
@@ -1965,6 +1966,12 @@ static void add_counts(hko_ctx* c, const Counts* k)
 static int omp_get_max_threads(void) { return 1; }
 #endif
 
+/* row y is computed (hko_set_stripes; every row otherwise) */
+static inline int row_on(const hko_ctx* c, int32_t y)
+{
+    return c->stripe_n < 2 || (y / 8) % c->stripe_n == c->stripe_k;
+}
+
 static void set_head(hko_ctx* c, uint32_t frame_number)
 {
     c->head = frame_number & 1u;
@@ -1999,7 +2006,10 @@ void hko_render_gbuffer(hko_ctx* c, const hk_frame_inputs* in)
         Counts k = {0, 0, 0};
 #pragma omp for schedule(dynamic, 4)
         for (int32_t y = c->band_y0; y < c->band_y1; ++y)
-            for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) gbuffer_pixel(c, &k, in, &G, x, y);
+            {
+                if (!row_on(c, y)) continue;
+                for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) gbuffer_pixel(c, &k, in, &G, x, y);
+            }
         add_counts(c, &k);
     }
     /* this frame's models are the next frame's previous ones */
@@ -2037,11 +2047,14 @@ static void run_pass(hko_ctx* c, const Pass* P, Kind kind)
         Counts k = {0, 0, 0};
 #pragma omp for schedule(dynamic, 4)
         for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
+        {
+            if (!row_on(c, y)) continue;
             for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) {
                 if (kind == K_DIRECT) direct_lit(P, &k, x, y);
                 else if (kind == K_INDIRECT) indirect_lit_ambient(P, &k, x, y);
                 else spatial_reuse(P, x, y);
             }
+        }
         add_counts(c, &k);
     }
 }
@@ -2059,7 +2072,10 @@ void hko_render_frame(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* 
     /* full-screen albedo over S */
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
     for (int32_t y = c->band_y0; y < c->band_y1; ++y)
-        for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) full_screen_albedo(&P, x, y);
+        {
+            if (!row_on(c, y)) continue;
+            for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) full_screen_albedo(&P, x, y);
+        }
 
     uint32_t current = P.number % 2u, previous = 1u - current;
     static const int pairs[3][2] = {{0, 4}, {2, 4}, {6, 8}};
@@ -2106,12 +2122,18 @@ void hko_denoise(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
         D.level = 0;
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
         for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
-            for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) demodulation(&D, x, y);
+            {
+                if (!row_on(c, y)) continue;
+                for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) demodulation(&D, x, y);
+            }
         for (int level = 0; level < 4; ++level) {
             D.level = level;
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
             for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
-                for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) denoise_pixel(&D, x, y);
+                {
+                    if (!row_on(c, y)) continue;
+                    for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) denoise_pixel(&D, x, y);
+                }
         }
     }
 }
@@ -2125,6 +2147,7 @@ void hko_tone_sum(hko_ctx* c, const hk_settings* st)
     size_t n = (size_t)c->s[0] * c->s[1];
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
     for (long long p = 0; p < (long long)n; ++p) {
+        if (!row_on(c, (int32_t)(p / (long long)c->s[0]))) continue;
         v4 col = load_rgba16f(d, (uint32_t)p);
         v4 ec = load_rgba16f(e, (uint32_t)p);
         col = V4(col.x + ec.x, col.y + ec.y, col.z + ec.z, col.w + ec.w);
@@ -2244,6 +2267,12 @@ void hko_set_band(hko_ctx* c, int32_t y0, int32_t rows, int32_t halo)
     int32_t a = y0 - halo, b = y0 + rows + halo;
     c->band_y0 = a < 0 ? 0 : a;
     c->band_y1 = b > (int32_t)c->S[1] ? (int32_t)c->S[1] : b;
+}
+
+void hko_set_stripes(hko_ctx* c, int32_t rank, int32_t world)
+{
+    c->stripe_n = world;
+    c->stripe_k = rank;
 }
 
 void hko_counters(hko_ctx* c, hk_counters* out) { *out = c->counters; }

@@ -34,6 +34,7 @@ def lib() -> C.CDLL:
         "hko_create": (vp, [vp, vp, u32, u32, f, C.c_int]),
         "hko_destroy": (None, [vp]),
         "hko_set_band": (None, [vp, C.c_int32, C.c_int32, C.c_int32]),
+        "hko_set_stripes": (None, [vp, C.c_int32, C.c_int32]),
         "hko_render_gbuffer": (None, [vp, vp]),
         "hko_set_scene": (None, [vp, vp]),
         "hko_render_frame": (None, [vp, vp, vp]),
@@ -117,6 +118,10 @@ class Oracle:
 
     def set_band(self, y0: int, rows: int, halo: int = 40):
         self._L.hko_set_band(self.ctx, y0, rows, halo)
+
+    def set_stripes(self, rank: int, world: int):
+        """Compute only this rank's 8-row stripes (hk_resize_striped's rows)."""
+        self._L.hko_set_stripes(self.ctx, rank, world)
 
     def post_process(self, settings, inputs):
         self._L.hko_post_process(self.ctx, C.byref(settings), C.byref(inputs))

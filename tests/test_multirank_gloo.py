@@ -1,13 +1,15 @@
-"""N>1 path on CPU: world_size-2 gloo ranks each render their row band (+ halo) with the oracle,
-all-gather the tone-mapped bands, and must reproduce the whole-frame render bit-exactly
-(bands.py halo sufficiency + the gather wiring that bench.py uses with RCCL on GPUs)."""
+"""N>1 path on CPU: world_size-2 and -4 gloo ranks each render only their own rows with the oracle —
+a row band + halo (hko_set_band) or their interleaved 8-row stripes (hko_set_stripes) — all-gather
+the tone-mapped rows, and must reproduce the whole-frame render bit-exactly (bands.py halo
+sufficiency + the gather wiring that bench.py uses with RCCL on GPUs).  The frame is 192 rows, so a
+band plus its 40-row halo on both sides is a strict part of it (96 + 80 and 48 + 80 rows)."""
 import os
 import socket
 
 import numpy as np
 import pytest
 
-W, H, FRAMES = 40, 48, 4
+W, H, FRAMES = 48, 192, 4
 
 
 def _free_port():
@@ -18,7 +20,7 @@ def _free_port():
     return p
 
 
-def _render(band=None, halo=40, spatial=True, denoise=True):
+def _render(band=None, halo=40, spatial=True, denoise=True, stripes=None, counters=False):
     from oracle import Oracle
 
     from hikari_amd import HikariSettings, Upscale, examples, frame_inputs, load_noise
@@ -29,20 +31,21 @@ def _render(band=None, halo=40, spatial=True, denoise=True):
     o = Oracle(desc, load_noise(), W, H, 1.0, threads=2)
     if band is not None:
         o.set_band(band.y0, band.rows, halo)
+    if stripes is not None:
+        o.set_stripes(*stripes)
     for f in range(FRAMES):
         fi = frame_inputs(f, cam, lights, W, H)
         o.render_gbuffer(fi)
         o.render_frame(s, fi)
         o.denoise(s, fi)
         o.tone_sum(s)
-    return o.output(10)
+    return (o.output(10), o.counters()) if counters else o.output(10)
 
 
 def _stripe_worker(rank, world, port, q):
-    """bench.py's stripe wiring: each rank contributes its (zero-padded) stripe rows, the gather
-    is reassembled with stripe_gather_rows' index.  No pass reads neighbours in this mode, so a
-    rank's stripe rows are the whole-frame render's rows (the GPU test checks the striped
-    contexts themselves)."""
+    """bench.py's stripe wiring: each rank renders only its stripes (an oracle context restricted to
+    them, as hk_resize_striped restricts a GPU context), contributes its (zero-padded) stripe rows,
+    and the gather is reassembled with stripe_gather_rows' index."""
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parent.parent
@@ -55,32 +58,39 @@ def _stripe_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    img = _render(None, 0, False, False)
+    img, cnt = _render(None, 0, False, False, stripes=(rank, world), counters=True)
     pad, index = stripe_gather_rows(world, H)
     mine = np.zeros((pad, W, 8), np.uint8)
     rows = stripe_rows(rank, world, H)
     mine[:len(rows)] = img[rows]
     full = torch.empty((world * pad, W, 8), dtype=torch.uint8)
     dist.all_gather_into_tensor(full, torch.from_numpy(mine))
+    n = torch.tensor([cnt["traverse_top"], cnt["traverse_emitter"], cnt["primary"]], dtype=torch.int64)
+    dist.all_reduce(n)
     if rank == 0:
-        q.put(full.numpy()[index].copy())
+        q.put((full.numpy()[index].copy(), n.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_stripes_reassemble_whole_frame():
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_stripes_reassemble_whole_frame(world):
+    """Each rank computes only its stripes; the gathered frame equals the whole-frame render and the
+    ranks' ray counts add up to the whole frame's (every pixel traced exactly once)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_stripe_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_stripe_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    gathered = q.get(timeout=300)
+    gathered, counts = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert np.array_equal(gathered, _render(None, 0, False, False))
+    whole, c = _render(None, 0, False, False, counters=True)
+    assert np.array_equal(gathered, whole)
+    assert counts == [c["traverse_top"], c["traverse_emitter"], c["primary"]]
 
 
 @pytest.mark.parametrize("world,height", [(1, 48), (2, 48), (3, 100), (8, 1080), (8, 2160), (5, 7)])
@@ -122,13 +132,17 @@ def _worker(rank, world, port, spatial, denoise, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("spatial,denoise", [(True, True), (False, False)])
-def test_two_rank_bands_reassemble_whole_frame(spatial, denoise):
+def test_rank_bands_reassemble_whole_frame(world, spatial, denoise):
     import torch.multiprocessing as mp
+    from hikari_amd.bands import band_of, halo_rows
+    b = band_of(0, world, H)
+    assert b.rows + 2 * halo_rows(True, True) < H  # a band + halo is a strict part of the frame
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, spatial, denoise, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, spatial, denoise, q)) for r in range(world)]
     for p in procs:
         p.start()
     gathered = q.get(timeout=300)
