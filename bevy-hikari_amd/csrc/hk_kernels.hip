@@ -274,7 +274,11 @@ __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
 }
 
 // ------------------------------------------------------------------ direct_lit (light.wgsl:1044-1261)
-template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE>
+// VALIDATE: 0 = the host knows this frame is not a validation frame of the pass (frame.number %
+// validate_interval != 0, light.wgsl:1096,1149), so the validation block is compiled out — it holds
+// the register peak (the reservoir stays live across its two walks: 142 -> 116 VGPRs for the emissive
+// pass, 3 -> 4 waves per SIMD) — and the candidate block always runs; 1 = the general body.
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true>
 HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top, uint32_t& n_emitter)
 {
     const Frame& F = A.F;
@@ -322,7 +326,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     const uint32_t validate_interval = EMISSIVE_LIT ? F.emissive_validate_interval : F.direct_validate_interval;
     const uint32_t select_light_instance = EMISSIVE_LIT ? im_x : DONT_SAMPLE_EMISSIVE;
 
-    if (umod(F.number, validate_interval) != 0u || r.count < 4.0f) {
+    if (!VALIDATE || umod(F.number, validate_interval) != 0u || r.count < 4.0f) {
         LightCandidate cand = select_light_candidate<true>(sc, F, s.random, xyz(s.visible_position), s.visible_normal,
                                                            select_light_instance, info, n_emitter);
         ray.origin = xyz(position) + normal * RAY_BIAS;
@@ -343,7 +347,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
         temporal_restir(r, s, w_new, F.max_temporal_reuse_count);
     }
 
-    if (umod(F.number, validate_interval) == 0u) {
+    if (VALIDATE && umod(F.number, validate_interval) == 0u) {
         LightCandidate cand = select_light_candidate<true>(sc, F, r.s.random, xyz(r.s.visible_position),
                                                            r.s.visible_normal, select_light_instance, info, n_emitter);
         ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
@@ -394,7 +398,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     store_rgba16f(C.render, idx, mk4(out.x, out.y, out.z, 1.0f));
 }
 
-template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS>
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, ChannelArgs C)
 {
     Scene sc;
@@ -403,7 +407,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_body<EMISSIVE_LIT, RENDER_EMISSIVE>(A, sc, C, x, y, n_top, n_emitter);
+        direct_body<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
 #define HK_DIRECT_LIT_W4 1
 #endif
 constexpr size_t DIRECT_LIT_W4_MIN_PX = 400000;
-template <bool LDS>
+template <bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_lit_w4(FrameArgs A, ChannelArgs C)
 {
     Scene sc;
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_body<false, true>(A, sc, C, x, y, n_top, n_emitter);
+        direct_body<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // only at their own pixel when the reprojection is the identity (zero velocity at upscale ratio
 // 1: the G-buffer of k_gbuffer), so per-thread program order is the reference's pass order for
 // every stored word; the runtime uses it only then.  One launch and one tail instead of two.
-template <bool LDS>
+template <bool LDS, bool VD, bool VE>
 __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A, ChannelArgs C0, ChannelArgs C1)
 {
     Scene sc;
@@ -446,8 +450,29 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
-        direct_body<false, true>(A, sc, C0, x, y, n_top, n_emitter);
-        direct_body<true, false>(A, sc, C1, x, y, n_top, n_emitter);
+        direct_body<false, true, VD>(A, sc, C0, x, y, n_top, n_emitter);
+        direct_body<true, false, VE>(A, sc, C1, x, y, n_top, n_emitter);
+    }
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
+// The fused launch on frames that are not emissive-validation frames, held to 4 waves per SIMD
+// (128 VGPRs): without the emissive validation block the body needs 117-137 VGPRs (the direct
+// validation block on every third frame), a few of which then spill.
+template <bool LDS, bool VD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_fused_w4(FrameArgs A, ChannelArgs C0,
+                                                                                                   ChannelArgs C1)
+{
+    Scene sc;
+    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+    else sc = A.sc;
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
+        direct_body<false, true, VD>(A, sc, C0, x, y, n_top, n_emitter);
+        direct_body<true, false, false>(A, sc, C1, x, y, n_top, n_emitter);
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -850,7 +875,7 @@ HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t
     return load_depth(F, G, x, y);
 }
 
-template <bool EMISSIVE_LIT>
+template <bool EMISSIVE_LIT, bool WINDOW>
 HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y, const DepthWin& W)
 {
     const Frame& F = A.F;
@@ -899,7 +924,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         f2 offset = mk2(py * cs, py * sn);
         int32_t scx = f2i32(offset.x + (float)x), scy = f2i32(offset.y + (float)y);
         int32_t sdx, sdy;
-        if (W.lds) {
+        if (WINDOW) {
             // upscale ratio 1 and s == S (the window variant): the uv bounds test is the integer
             // test (see k_denoise3), and jittered_coords(coords_to_uv(c)) == c: the jitter is
             // (j * tx) * 0 and u32((c + 0.5) / S * S) truncates back to c for c < 2^22
@@ -914,23 +939,42 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         float sample_depth = win_depth(F, A.G, W, sdx, sdy);
         float depth_ratio = depth / sample_depth;
         if (depth_ratio < 0.9f || depth_ratio > 1.1f) continue;
-        q = load_res(C.cur, s_index(F, scx, scy));
-        bool normal_miss = dot(s.visible_normal, q.s.visible_normal) < 0.866f;
-        if (q.count < HK_F32_EPSILON || normal_miss) continue;
-        f3 sample_direction = normalize(xyz(q.s.sample_position) - xyz(s.visible_position));
+        // the neighbour's reservoir, its 16-byte planes loaded as the tests need them (the rejection
+        // tests read plane 3 (count, normals) and plane 2 (sample position); planes 0-1 only for a
+        // neighbour that is merged): the same values as load_res, fewer gathers for rejected ones
+        const int32_t nidx = s_index(F, scx, scy);
+        const uint4 c3 = C.cur.base[3u * C.cur.n + (uint32_t)nidx];
+        const float q_count = unpack_lo16float(c3.z);
+        const f3 q_normal = normalize(mk3(hk_unpack_snorm8(c3.x, 0), hk_unpack_snorm8(c3.x, 1), hk_unpack_snorm8(c3.x, 2)));
+        bool normal_miss = dot(s.visible_normal, q_normal) < 0.866f;
+        if (q_count < HK_F32_EPSILON || normal_miss) continue;
+        const uint4 c2 = C.cur.base[2u * C.cur.n + (uint32_t)nidx];
+        const f3 q_sample = mk3(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z));
+        f3 sample_direction = normalize(q_sample - xyz(s.visible_position));
         if (dot(sample_direction, s.visible_normal) < 0.0f) continue;
 
         const float tap_interval = F.sp_tap_interval[EMISSIVE_LIT][i - 1u];  // max(1, py / 5)
-        const uint32_t tap_count = F.sp_tap_count[EMISSIVE_LIT][i - 1u];    // u32(py / tap_interval)
+        uint32_t tap_count = F.sp_tap_count[EMISSIVE_LIT][i - 1u];          // u32(py / tap_interval)
         bool occluded = false;
+#ifdef HK_EXPERIMENT_SP_NO_MARCH  // timing experiments only (break parity)
+        tap_count = 0u;
+#endif
         float inv_len = 1.0f / sqrtf(dot(offset, offset));
         f2 dir = mk2(offset.x * inv_len, offset.y * inv_len);
+        const float sx = (float)F.s[0], sy = (float)F.s[1];
         for (uint32_t j = 1u; j <= tap_count; j += 1u) {
             float tap_dist = (float)j * tap_interval;
-            f2 tuv = mk2(uv.x + div_by(tap_dist * dir.x, (float)F.s[0], F.inv_s[0]),
-                         uv.y + div_by(tap_dist * dir.y, (float)F.s[1], F.inv_s[1]));
+            f2 tuv = mk2(uv.x + div_by(tap_dist * dir.x, sx, F.inv_s[0]), uv.y + div_by(tap_dist * dir.y, sy, F.inv_s[1]));
             int32_t tdx, tdy;
-            jittered_coords(F, tuv, tdx, tdy);
+            if constexpr (WINDOW) {
+                // ratio 1, s == S: jittered_coords(tuv) adds the jitter (j tx) * 0 = +-0 to tuv (never -0
+                // itself: uv > 0 and an exact cancellation rounds to +0), so it is i32(tuv * S); tuv is
+                // finite and within [-1, 2], where the plain conversion is f2i32's value
+                tdx = (int32_t)(tuv.x * sx);
+                tdy = (int32_t)(tuv.y * sy);
+            } else {
+                jittered_coords(F, tuv, tdx, tdy);
+            }
             float tap_depth = win_depth(F, A.G, W, tdx, tdy);
             // j / (tap_count + 1) from the host table (tap_count <= 5 for RANGE <= 20)
             const float t = tap_count < 7u && j < 6u ? F.sp_tap_t[tap_count][j] : (float)j / (float)(tap_count + 1u);
@@ -941,6 +985,10 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             }
         }
         if (occluded) continue;
+        q = unpack_reservoir(C.cur.base[(uint32_t)nidx], C.cur.base[C.cur.n + (uint32_t)nidx], c2, c3);
+#ifdef HK_EXPERIMENT_SP_NO_SHADE
+        merge_reservoir(r, q, q.s.radiance.x);
+#else
         float jacobian = q.s.sample_position.w > 0.5f ? compute_jacobian(q.s, s) : 1.0f;
         if (EMISSIVE_LIT) {
             merge_reservoir(r, q, lum(xyz(q.s.radiance)) / jacobian);
@@ -948,6 +996,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             f3 o = shade(sc, sample_direction, q.s.radiance);
             merge_reservoir(r, q, lum(o) / jacobian);
         }
+#endif
     }
     float m = (float)F.max_spatial_reuse_count;
     if (r.count > m) {
@@ -981,7 +1030,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_spatial(FrameArgs A, Chann
         W.lds = win;
     }
     int32_t x, y;
-    if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT>(A, C, x, y, W);
+    if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT, WINDOW>(A, C, x, y, W);
 }
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
@@ -1219,29 +1268,58 @@ void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st)
 {
     hipLaunchKernelGGL(k_albedo, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, albedo);
 }
+// a validation frame of a direct-light pass: frame.number % interval == 0 (umod: interval 0 -> 0)
+static bool validation_frame(uint32_t number, uint32_t interval) { return interval == 0u || number % interval == 0u; }
+template <bool EL, bool RE, bool LDS>
+static void launch_direct_v(const FrameArgs& A, const ChannelArgs& C, bool val, dim3 g, uint32_t lds, hipStream_t st)
+{
+    if (val) hipLaunchKernelGGL((k_direct<EL, RE, LDS, true>), g, dim3(256), lds, st, A, C);
+    else hipLaunchKernelGGL((k_direct<EL, RE, LDS, false>), g, dim3(256), lds, st, A, C);
+}
 void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
 {
     dim3 g = tiles(A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
     if (emissive_lit) {
-        if (lds) hipLaunchKernelGGL((k_direct<true, false, true>), g, dim3(256), lds, st, A, C);
-        else hipLaunchKernelGGL((k_direct<true, false, false>), g, dim3(256), 0, st, A, C);
+        const bool val = validation_frame(A.F.number, A.F.emissive_validate_interval);
+        if (lds) launch_direct_v<true, false, true>(A, C, val, g, lds, st);
+        else launch_direct_v<true, false, false>(A, C, val, g, 0, st);
     } else {
+        const bool val = validation_frame(A.F.number, A.F.direct_validate_interval);
         const char* wmin = getenv("HK_DIRECT_W4_MIN_PX");  // read per launch: tests force either kernel
         const double w4_min = wmin ? atof(wmin) : (double)DIRECT_LIT_W4_MIN_PX;
         if (HK_DIRECT_LIT_W4 && (double)A.F.s[0] * (double)A.F.s_rows >= w4_min) {
-            if (lds) hipLaunchKernelGGL(k_direct_lit_w4<true>, g, dim3(256), lds, st, A, C);
-            else hipLaunchKernelGGL(k_direct_lit_w4<false>, g, dim3(256), 0, st, A, C);
-        } else if (lds) hipLaunchKernelGGL((k_direct<false, true, true>), g, dim3(256), lds, st, A, C);
-        else hipLaunchKernelGGL((k_direct<false, true, false>), g, dim3(256), 0, st, A, C);
+            if (lds) {
+                if (val) hipLaunchKernelGGL((k_direct_lit_w4<true, true>), g, dim3(256), lds, st, A, C);
+                else hipLaunchKernelGGL((k_direct_lit_w4<true, false>), g, dim3(256), lds, st, A, C);
+            } else {
+                if (val) hipLaunchKernelGGL((k_direct_lit_w4<false, true>), g, dim3(256), 0, st, A, C);
+                else hipLaunchKernelGGL((k_direct_lit_w4<false, false>), g, dim3(256), 0, st, A, C);
+            }
+        } else if (lds) launch_direct_v<false, true, true>(A, C, val, g, lds, st);
+        else launch_direct_v<false, true, false>(A, C, val, g, 0, st);
     }
+}
+template <bool LDS>
+static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, bool vd, bool ve, dim3 g,
+                           uint32_t lds, hipStream_t st)
+{
+    static const bool w4 = !getenv("HK_NO_FUSED_W4");
+    if (vd && ve) hipLaunchKernelGGL((k_direct_fused<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
+    else if (ve) hipLaunchKernelGGL((k_direct_fused<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
+    else if (w4 && vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true>), g, dim3(256), lds, st, A, C0, C1);
+    else if (w4) hipLaunchKernelGGL((k_direct_fused_w4<LDS, false>), g, dim3(256), lds, st, A, C0, C1);
+    else if (vd) hipLaunchKernelGGL((k_direct_fused<LDS, true, false>), g, dim3(256), lds, st, A, C0, C1);
+    else hipLaunchKernelGGL((k_direct_fused<LDS, false, false>), g, dim3(256), lds, st, A, C0, C1);
 }
 void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, hipStream_t st)
 {
     dim3 g = tiles(A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
-    if (lds) hipLaunchKernelGGL(k_direct_fused<true>, g, dim3(256), lds, st, A, C0, C1);
-    else hipLaunchKernelGGL(k_direct_fused<false>, g, dim3(256), 0, st, A, C0, C1);
+    const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
+    const bool ve = validation_frame(A.F.number, A.F.emissive_validate_interval);
+    if (lds) launch_fused_v<true>(A, C0, C1, vd, ve, g, lds, st);
+    else launch_fused_v<false>(A, C0, C1, vd, ve, g, 0, st);
 }
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st)
 {

@@ -468,7 +468,7 @@ def test_gpu_instance_update_matches_host_rebuild(scene_fn):
     from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
     from oracle import Oracle
     scene0, cam, lights = examples.SCENES[scene_fn]()
-    scene0.build()
+    d0 = scene0.build()
     r = HikariRenderer(0)
     r.set_noise()
     r.upload_scene(scene0)
@@ -497,10 +497,16 @@ def test_gpu_instance_update_matches_host_rebuild(scene_fn):
     leaf_ids = h["entry"][~inner] - 0x80000000
     assert np.array_equal(g["min"][~inner], inst[leaf_ids, 0:3]) and np.array_equal(g["max"][~inner], inst[leaf_ids, 4:7])
     # and the frame
+    from test_gpu_motion import _compare as compare_with_motion
     w, hgt = 48, 32
-    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=False)
     r.resize(w, hgt, 1.0)
-    o = Oracle(d1, load_noise(), w, hgt, 1.0)
+    # the oracle sees the same history: the uploaded scene, then the moved one (the first frame's
+    # motion vectors reproject from the uploaded models, GlobalTransformQueue); single-threaded and
+    # with spatial reuse off, as the reprojection scatter into the spatial pair is a write race
+    # (test_gpu_motion.py)
+    o = Oracle(d0, load_noise(), w, hgt, 1.0, threads=1)
+    o.set_scene(d1)
     s = st.to_c()
     errors = []
     for f in range(2):
@@ -510,7 +516,7 @@ def test_gpu_instance_update_matches_host_rebuild(scene_fn):
             x.render_frame(s, fi)
             x.denoise(s, fi)
             x.tone_sum(s)
-        _compare_frame(r, o, f, errors)
+        compare_with_motion(r, o, f, errors)
     assert not errors, "\n".join(errors[:10])
 
 
