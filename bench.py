@@ -56,7 +56,9 @@ BYTES_PER_PIXEL = {
     "indirect_wavefront": 184,       # the same compulsory streams (queues / hit records are extra traffic)
     "indirect_spatial_reuse": 244,   # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8
     "emissive_spatial_reuse": 244,
-    "demodulation": 92,              # 3 channels x (render 8 + variance 4 + internal 8 + ivar 4) + albedo 8 + G 12 + geom 32
+    "demodulation": 148,             # reads G-buffer normal 4 + position 16 (RGBA32F texel, .w used) + ids 8 +
+                                     # depth gradient 8 + albedo 8 + 3 x (render 8 + variance 4); writes geom 32
+                                     # (the levels' per-pixel geometry) + 3 x (internal 8 + ivar 4)
     "denoise": 120,                  # geom 32 + 3 x (ivar 4 + input 8 + output 8) (+ albedo 8 at L3)
     "tone_mapping": 32,
 }

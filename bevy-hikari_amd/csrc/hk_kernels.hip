@@ -916,7 +916,13 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 
     const float rf = hk_random_float(F.number);
     const float srand = sum4(s.random);
+#if defined(HK_LANE_STATS) && defined(HK_SP_STATS)
+    LaneStats lane_stats_;
+#endif
     for (uint32_t i = 1u; i <= COUNT; i += 1u) {
+#if defined(HK_LANE_STATS) && HK_SP_STATS == 0  // lane statistics per neighbour iteration (experiments)
+        lane_stats_.tick();
+#endif
         float px = HK_TAU * hk_fract(((float)i * HK_GOLDEN_RATIO + srand) + rf);
         const float py = F.sp_py[EMISSIVE_LIT][i - 1u];  // sqrt(i / COUNT) * RANGE
         float sn, cs;
@@ -956,6 +962,9 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         const float tap_interval = F.sp_tap_interval[EMISSIVE_LIT][i - 1u];  // max(1, py / 5)
         uint32_t tap_count = F.sp_tap_count[EMISSIVE_LIT][i - 1u];          // u32(py / tap_interval)
         bool occluded = false;
+#if defined(HK_LANE_STATS) && HK_SP_STATS == 1  // lane statistics at the occlusion march (experiments)
+        lane_stats_.tick();
+#endif
 #ifdef HK_EXPERIMENT_SP_NO_MARCH  // timing experiments only (break parity)
         tap_count = 0u;
 #endif
@@ -985,6 +994,9 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             }
         }
         if (occluded) continue;
+#if defined(HK_LANE_STATS) && HK_SP_STATS == 2  // lane statistics at the merge (experiments)
+        lane_stats_.tick();
+#endif
         q = unpack_reservoir(C.cur.base[(uint32_t)nidx], C.cur.base[C.cur.n + (uint32_t)nidx], c2, c3);
 #ifdef HK_EXPERIMENT_SP_NO_SHADE
         merge_reservoir(r, q, q.s.radiance.x);
