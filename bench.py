@@ -50,7 +50,8 @@ BYTES_PER_PIXEL = {
     "full_screen_albedo": 52,        # reads 44 B of G-buffer, writes RGBA16F
     "direct_lit": 184,               # G 44 + reservoir read 64 + write 64 + variance 4 + render 8
     "direct_emissive": 184,
-    "direct_lit_emissive": 368,      # both passes in one launch (k_direct_fused)
+    "direct_lit_emissive": 324,      # both passes in one launch (k_direct_fused): the G-buffer read once,
+                                     # 2 x (reservoir read 64 + write 64 + variance 4 + render 8)
     "indirect_lit_ambient": 184,
     "indirect_multiple_bounces": 184,
     "indirect_wavefront": 184,       # the same compulsory streams (queues / hit records are extra traffic)

@@ -1645,6 +1645,18 @@ static const float HALTON[8][4] = { /* view.rs:130-139 */
     {0.062500f, 0.888889f, 0.562500f, 0.037037f}, {0.312500f, 0.370370f, 0.812500f, 0.703704f},
     {0.187500f, 0.148148f, 0.687500f, 0.481481f}, {0.437500f, 0.814815f, 0.937500f, 0.259259f}};
 
+/* frame_jitter (prepass.wgsl:30-38) */
+static void frame_jitter(const hk_frame_inputs* in, float* jitter)
+{
+    jitter[0] = jitter[1] = 0.0f;
+    if (in->jitter == HK_JITTER_TAA || in->jitter == HK_JITTER_TAA_SMAA) {
+        uint32_t index = in->jitter == HK_JITTER_TAA_SMAA ? (in->frame_number >> 1) & 15u : in->frame_number & 15u;
+        const float* h = HALTON[index >> 1];
+        jitter[0] = (index & 1u) == 0u ? h[0] : h[2];
+        jitter[1] = (index & 1u) == 0u ? h[1] : h[3];
+    }
+}
+
 static void gbuffer_pixel(const hko_ctx* c, Counts* cnt, const hk_frame_inputs* in, const GbFrame* G, int32_t x,
                           int32_t y)
 {
@@ -1989,14 +2001,7 @@ void hko_render_gbuffer(hko_ctx* c, const hk_frame_inputs* in)
     c->g_prev_velocity_uv = t;
     set_head(c, in->frame_number);
     GbFrame G;
-    G.jitter[0] = G.jitter[1] = 0.0f;
-    if (in->jitter == HK_JITTER_TAA || in->jitter == HK_JITTER_TAA_SMAA) {
-        /* frame_jitter (prepass.wgsl:30-38) */
-        uint32_t index = in->jitter == HK_JITTER_TAA_SMAA ? (in->frame_number >> 1) & 15u : in->frame_number & 15u;
-        const float* h = HALTON[index >> 1];
-        G.jitter[0] = (index & 1u) == 0u ? h[0] : h[2];
-        G.jitter[1] = (index & 1u) == 0u ? h[1] : h[3];
-    }
+    frame_jitter(in, G.jitter);
     G.previous_view_proj = in->has_previous_view ? in->previous_view_proj : in->view.view_proj;
     G.motion = memcmp(G.previous_view_proj, in->view.view_proj, 64) != 0;
     for (uint32_t i = 0; i < c->n_instances && !G.motion; ++i)
@@ -2304,6 +2309,30 @@ void hko_trace(hko_ctx* c, const float* rays, const float* max_distance, const f
         if (hko_steps_out) hko_steps_out[i] = hko_ray_steps;
 #endif
     }
+}
+
+/* Primary rays of frame `in` (jittered as the G-buffer pass) walked two ways: the G-buffer's
+ * ordered closest-hit walk and the reference-order traverse_top (light.wgsl:400-486, no early
+ * exit).  out = 6 words per pixel: (instance, primitive, distance bits) of each walk. */
+void hko_primary_hits(hko_ctx* c, const hk_frame_inputs* in, uint32_t* out)
+{
+    float jitter[2];
+    frame_jitter(in, jitter);
+#pragma omp parallel for schedule(dynamic, 4) HKO_THREADS(c)
+    for (long long y = 0; y < (long long)c->S[1]; ++y)
+        for (uint32_t x = 0; x < c->S[0]; ++x) {
+            Ray ray;
+            ray.origin = ld3(in->view.world_position);
+            ray.direction = primary_direction(&in->view, ((float)x + 0.5f) - jitter[0],
+                                              ((float)y + 0.5f) - jitter[1], c->S);
+            ray.inv_direction = inv3(ray.direction);
+            Counts k = {0, 0, 0};
+            Hit a = closest_hit_ordered(c, &ray);
+            Hit b = traverse_top(c, &k, &ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+            uint32_t* o = out + 6 * ((size_t)y * c->S[0] + x);
+            o[0] = a.instance_index; o[1] = a.primitive_index; o[2] = hk_f2u(a.intersection.distance);
+            o[3] = b.instance_index; o[4] = b.primitive_index; o[5] = hk_f2u(b.intersection.distance);
+        }
 }
 
 /* ---- KAT exports ---- */

@@ -57,6 +57,7 @@ void hko_counters(hko_ctx* ctx, hk_counters* out);
 void hko_reset_counters(hko_ctx* ctx);
 
 /* light.wgsl:442-486 for n rays {origin, direction}; hits {u, v, t, instance, primitive} */
+void hko_primary_hits(hko_ctx* ctx, const hk_frame_inputs* in, uint32_t* out);
 void hko_trace(hko_ctx* ctx, const float* rays, const float* max_distance, const float* early_distance,
                const uint32_t* exclude_instance, uint32_t n, void* hits);
 

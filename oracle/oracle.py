@@ -45,6 +45,7 @@ def lib() -> C.CDLL:
         "hko_counters": (None, [vp, vp]),
         "hko_reset_counters": (None, [vp]),
         "hko_trace": (None, [vp, vp, vp, vp, vp, u32, vp]),
+        "hko_primary_hits": (None, [vp, vp, vp]),
         "hko_intersects_aabb": (f, [vp, vp, vp, vp]),
         "hko_intersects_triangle": (None, [vp, vp, vp, vp, vp, vp]),
         "hko_pack_reservoir_roundtrip": (None, [vp, vp, vp]),
@@ -163,6 +164,12 @@ class Oracle:
 
     def reset_counters(self):
         self._L.hko_reset_counters(self.ctx)
+
+    def primary_hits(self, frame_inputs) -> np.ndarray:
+        """(h, w, 2, 3) words: [ordered walk, reference-order walk] x (instance, primitive, distance bits)."""
+        out = np.empty((self.height, self.width, 2, 3), np.uint32)
+        self._L.hko_primary_hits(self.ctx, C.byref(frame_inputs), out.ctypes.data)
+        return out
 
     def trace(self, rays, max_distance=None, early_distance=None, exclude=None) -> np.ndarray:
         rays = np.ascontiguousarray(rays, np.float32)

@@ -18,14 +18,14 @@ from pathlib import Path
 
 SHORT = {  # mangled and demangled spellings
     "k_gbuffer": "gbuffer", "k_albedo": "full_screen_albedo",
-    "k_direct_fused": "direct_lit_emissive",
+    "k_direct_fused": "direct_lit_emissive", "k_direct_lit_w4": "direct_lit",
     "k_directILb0ELb1": "direct_lit", "k_direct<false, true": "direct_lit",
     "k_directILb1ELb0": "direct_emissive", "k_direct<true, false": "direct_emissive",
     "k_indirectILb0": "indirect_lit_ambient", "k_indirect<false": "indirect_lit_ambient",
     "k_indirectILb1": "indirect_multiple_bounces", "k_indirect<true": "indirect_multiple_bounces",
     "k_spatialILb0": "indirect_spatial_reuse", "k_spatial<false": "indirect_spatial_reuse",
     "k_spatialILb1": "emissive_spatial_reuse", "k_spatial<true": "emissive_spatial_reuse",
-    "k_demod3": "demodulation", "k_denoise3": "denoise", "k_tone": "tone_mapping", "k_trace": "trace",
+    "k_wf_": "indirect_wavefront", "k_demod3": "demodulation", "k_denoise3": "denoise", "k_tone": "tone_mapping", "k_trace": "trace",
     "k_f16": "f16_selftest", "k_build_wide": "scene_build_wide", "k_fill_blas_leaves": "scene_fill_leaves",
     "k_fill_tlas_leaves": "scene_fill_leaves", "k_collapse_decide": "scene_collapse_leaves",
     "k_collapse_write": "scene_collapse_leaves",
