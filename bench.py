@@ -313,7 +313,7 @@ def main():
     r.reset_counters()
     # per-kernel HIP events on every 4th frame of the timed region (frame_number % 4 == 0): the
     # averages the roofline needs, without event records perturbing the other frames
-    r.set_kernel_timing_interval(int(os.environ.get("HK_BENCH_TIMING_EVERY", "4")))
+    r.set_kernel_timing_interval(max(1, min(args.steps, int(os.environ.get("HK_BENCH_TIMING_EVERY", "4")))))
     r.enable_kernel_timing(True)
     torch.cuda.synchronize()
     if world > 1:

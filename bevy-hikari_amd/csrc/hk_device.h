@@ -173,6 +173,10 @@ struct Frame {
     uint32_t S[2], s[2];
     int32_t S_row0, S_rows;  // deferred-plane band
     int32_t s_row0, s_rows;  // integrator-plane band
+    // launch window (win_rows > 0): this launch covers only the local plane rows
+    // [win_row0, win_row0 + win_rows) — a band's passes shrink their halo rows pass by pass
+    // (hk_runtime.hip pass_window); 0: the whole plane
+    int32_t win_row0, win_rows;
     int32_t count_y0, count_y1;    // global integrator rows whose rays are counted (the band's own rows)
     int32_t count_Sy0, count_Sy1;  // the same for the full-resolution G-buffer rows
     // interleaved stripes (stripe_n >= 2): the local planes hold the STRIPE_H-row stripes

@@ -88,9 +88,11 @@ HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, 
     uint32_t t = threadIdx.x;
     uint32_t w = t >> 6, lane = t & 63u;
     x = (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
-    int32_t ly = (int32_t)(ty * 16u + (w >> 1) * 8u + (lane >> 3));
+    const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0;
+    const int32_t w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : rows;
+    int32_t ly = w0 + (int32_t)(ty * 16u + (w >> 1) * 8u + (lane >> 3));
     y = global_row(F, ly, row0);
-    return (uint32_t)x < width && ly < rows;
+    return (uint32_t)x < width && ly < w1;
 }
 
 // Occupancy hints for the traversal kernels (waves per SIMD); tunable at build time.
@@ -119,15 +121,23 @@ HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, 
 #else
 #define HK_INDIRECT_OCC HK_TRACE_OCC
 #endif
+#ifndef HK_SPATIAL_WAVES
+#define HK_SPATIAL_WAVES 0
+#endif
+#if HK_SPATIAL_WAVES > 0
+#define HK_SPATIAL_OCC __attribute__((amdgpu_waves_per_eu(HK_SPATIAL_WAVES, 8)))
+#else
+#define HK_SPATIAL_OCC HK_TRACE_OCC
+#endif
 
 // origin (global coordinates, contiguous bands) of this workgroup's tile
 template <int ORDER = RASTER>
-HKD void tile_origin(int32_t row0, int32_t& x0, int32_t& y0)
+HKD void tile_origin(const Frame& F, int32_t row0, int32_t& x0, int32_t& y0)
 {
     uint32_t tx, ty;
     tile_coords<ORDER>(tx, ty);
     x0 = (int32_t)(tx * 16u);
-    y0 = row0 + (int32_t)(ty * 16u);
+    y0 = row0 + (F.win_rows > 0 ? F.win_row0 : 0) + (int32_t)(ty * 16u);
 }
 #ifndef HK_SPATIAL_ORDER
 #define HK_SPATIAL_ORDER XCD_STRIPS
@@ -875,6 +885,14 @@ HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t
     return load_depth(F, G, x, y);
 }
 
+// The reservoir being built is carried through the neighbour loop as (count, w_sum, w2_sum) plus
+// the index of the record its sample came from (sel: a neighbour's index in `cur`, SEL_OWN or
+// SEL_PREVIOUS); the selected sample is re-read from that record once, after the loop.  The
+// records are not written by this pass (it writes C.spatial only), so the re-read returns the
+// bits update_reservoir() would have copied (light.wgsl:138-151), and the 22 registers of a
+// carried sample (plus the copy per merge) leave the loop.
+constexpr int32_t SEL_OWN = -1, SEL_PREVIOUS = -2;
+
 template <bool EMISSIVE_LIT, bool WINDOW>
 HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y, const DepthWin& W)
 {
@@ -887,35 +905,60 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     f4 pd = load_position(F, A.G, dx, dy);
     f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
     float depth = pd.w;
-    Reservoir r = load_res(C.cur, idx);
     if (depth < HK_F32_EPSILON) {
-        store_res(C.spatial, idx, r);
+        store_res(C.spatial, idx, load_res(C.cur, idx));
         store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
         return;
     }
+    const Reservoir own = load_res(C.cur, idx);
+    const Sample& s = own.s;
     uint32_t im_y = f2u32(load_instance_material(F, A.G, dx, dy).y);
     f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
     Surface surface = retreive_surface(A.sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
-    bool use_spatial_variance = r.count <= 4.0f;
+    const bool use_spatial_variance = own.count <= 4.0f;
     f2 juv = jittered_uv(F, uv, 0.25f);
     f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
-    Reservoir q = r;
-    const Sample s = q.s;
     float lifetime_max = F.max_reservoir_lifetime <= 1.0f ? HK_F32_MAX : F.max_reservoir_lifetime;
-    if (r.lifetime <= lifetime_max) r = load_previous(F, C.prev_spatial, previous_uv);
+    // r = the previous spatial reservoir (load_previous) or the pixel's own one
+    const bool from_previous = own.lifetime <= lifetime_max;
+    int32_t previous_index = -1;  // load_previous's record; -1: outside the frame (the zero reservoir)
+    if (from_previous && uv_inside_open(previous_uv))
+        previous_index = s_index(F, f2i32(previous_uv.x * (float)F.s[0]), f2i32(previous_uv.y * (float)F.s[1]));
+    float r_count = own.count, r_lifetime = own.lifetime, r_w_sum = own.w_sum, r_w2_sum = own.w2_sum;
+    int32_t sel = SEL_OWN;
+    if (from_previous) {
+        sel = SEL_PREVIOUS;
+        r_count = r_lifetime = r_w_sum = r_w2_sum = 0.0f;
+        if (previous_index >= 0) {
+            const uint4 p3 = C.prev_spatial.base[3u * C.prev_spatial.n + (uint32_t)previous_index];
+            r_count = unpack_lo16float(p3.z);
+            r_w_sum = unpack_lo16float(p3.w);
+            r_w2_sum = unpack_hi16float(p3.w);
+            r_lifetime = 127.0f * (1.0f + hk_unpack_snorm8(p3.x, 3));
+        }
+    }
     f3 view_direction = calculate_view(F, position);
     const ShadeCtx sc = shade_ctx(F, view_direction, s.visible_normal, surface);
+    // merge_reservoir(r, own, p) (light.wgsl:153-160)
+    auto merge = [&](float p, float q_w, float q_count, f4 q_random, int32_t q_sel) {
+        const float w_new = (p * q_w) * q_count;
+        r_w_sum += w_new;
+        r_w2_sum += w_new * w_new;
+        const float rand = hk_fract(sum4(q_random));
+        if (rand < w_new / r_w_sum) sel = q_sel;
+        r_count = r_count + q_count;
+    };
     if (EMISSIVE_LIT) {
-        merge_reservoir(r, q, lum(xyz(q.s.radiance)));
+        merge(lum(xyz(s.radiance)), own.w, own.count, s.random, SEL_OWN);
     } else {
         f3 o = shade(sc, normalize(xyz(s.sample_position) - xyz(s.visible_position)), s.radiance);
-        merge_reservoir(r, q, lum(o));
+        merge(lum(o), own.w, own.count, s.random, SEL_OWN);
     }
-    r.s.visible_position = s.visible_position;
-    r.s.visible_normal = s.visible_normal;
 
     const float rf = hk_random_float(F.number);
     const float srand = sum4(s.random);
+    const f3 s_visible = xyz(s.visible_position);
+    const f3 s_normal = s.visible_normal;
 #if defined(HK_LANE_STATS) && defined(HK_SP_STATS)
     LaneStats lane_stats_;
 #endif
@@ -952,12 +995,15 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         const uint4 c3 = C.cur.base[3u * C.cur.n + (uint32_t)nidx];
         const float q_count = unpack_lo16float(c3.z);
         const f3 q_normal = normalize(mk3(hk_unpack_snorm8(c3.x, 0), hk_unpack_snorm8(c3.x, 1), hk_unpack_snorm8(c3.x, 2)));
-        bool normal_miss = dot(s.visible_normal, q_normal) < 0.866f;
+        bool normal_miss = dot(s_normal, q_normal) < 0.866f;
         if (q_count < HK_F32_EPSILON || normal_miss) continue;
         const uint4 c2 = C.cur.base[2u * C.cur.n + (uint32_t)nidx];
         const f3 q_sample = mk3(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z));
-        f3 sample_direction = normalize(q_sample - xyz(s.visible_position));
-        if (dot(sample_direction, s.visible_normal) < 0.0f) continue;
+        // normalize(q_sample - visible), its length kept for the jacobian below
+        const f3 to_sample = q_sample - s_visible;
+        const float to_sample_length = sqrtf(dot(to_sample, to_sample));
+        f3 sample_direction = to_sample * rcp_exact(to_sample_length);
+        if (dot(sample_direction, s_normal) < 0.0f) continue;
 
         const float tap_interval = F.sp_tap_interval[EMISSIVE_LIT][i - 1u];  // max(1, py / 5)
         uint32_t tap_count = F.sp_tap_count[EMISSIVE_LIT][i - 1u];          // u32(py / tap_interval)
@@ -997,19 +1043,67 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 #if defined(HK_LANE_STATS) && HK_SP_STATS == 2  // lane statistics at the merge (experiments)
         lane_stats_.tick();
 #endif
-        q = unpack_reservoir(C.cur.base[(uint32_t)nidx], C.cur.base[C.cur.n + (uint32_t)nidx], c2, c3);
+        // merge_reservoir(r, q, p / jacobian): the fields of q that the merge reads
+        const uint4 c0 = C.cur.base[(uint32_t)nidx];
+        const float q_w = unpack_hi16float(c3.z);
+        const f4 q_radiance = mk4(unpack_lo16float(c0.x), unpack_hi16float(c0.x), unpack_lo16float(c0.y),
+                                  unpack_hi16float(c0.y));
+        const f4 q_random = mk4(hk_unpack_unorm16(c0.z), hk_unpack_unorm16(c0.z >> 16), hk_unpack_unorm16(c0.w),
+                                hk_unpack_unorm16(c0.w >> 16));
 #ifdef HK_EXPERIMENT_SP_NO_SHADE
-        merge_reservoir(r, q, q.s.radiance.x);
+        merge(q_radiance.x, q_w, q_count, q_random, nidx);
 #else
-        float jacobian = q.s.sample_position.w > 0.5f ? compute_jacobian(q.s, s) : 1.0f;
+        float jacobian = 1.0f;
+        if (hk_unpack_snorm8(c3.y, 3) > 0.5f) {
+            // compute_jacobian(q.s, s) (light.wgsl:990-1004).  Its first vector, visible - q_sample,
+            // is -to_sample exactly, so its normalisation is -sample_direction and its length is
+            // to_sample_length, bit for bit (negation is exact; the squares are equal)
+            const uint4 c1 = C.cur.base[C.cur.n + (uint32_t)nidx];
+            const f3 q_visible = mk3(__uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z));
+            const f3 normal = normalize(mk3(hk_unpack_snorm8(c3.y, 0), hk_unpack_snorm8(c3.y, 1), hk_unpack_snorm8(c3.y, 2)));
+            const float c1_ = fabsf(dot(sample_direction, normal));
+            const f3 back = q_visible - q_sample;
+            const float back_length = sqrtf(dot(back, back));
+            const float c2_ = fabsf(dot(back * rcp_exact(back_length), normal));
+            const float term_1 = c1_ / fmaxf(0.0001f, c2_);
+            const float num = back_length * back_length;
+            const float denom = to_sample_length * to_sample_length;
+            const float term_2 = num / fmaxf(denom, 0.0001f);
+            jacobian = hk_clampf(term_1 * term_2, 1.0f, 50.0f);
+        }
         if (EMISSIVE_LIT) {
-            merge_reservoir(r, q, lum(xyz(q.s.radiance)) / jacobian);
+            merge(lum(xyz(q_radiance)) / jacobian, q_w, q_count, q_random, nidx);
         } else {
-            f3 o = shade(sc, sample_direction, q.s.radiance);
-            merge_reservoir(r, q, lum(o) / jacobian);
+            f3 o = shade(sc, sample_direction, q_radiance);
+            merge(lum(o) / jacobian, q_w, q_count, q_random, nidx);
         }
 #endif
     }
+    // the selected sample, re-read from its record (see SEL_OWN above)
+    Reservoir r;
+    {
+        const uint4* base = C.cur.base;
+        uint32_t n = C.cur.n;
+        int32_t at = sel >= 0 ? sel : idx;
+        if (sel == SEL_PREVIOUS) {
+            base = C.prev_spatial.base;
+            n = C.prev_spatial.n;
+            at = previous_index;
+        }
+        if (at >= 0) {
+            r = unpack_reservoir(base[at], base[n + (uint32_t)at], base[2u * n + (uint32_t)at], base[3u * n + (uint32_t)at]);
+        } else {
+            r = zero_reservoir();
+        }
+        if (sel < 0) {  // r.s.visible_position / visible_normal = s's (light.wgsl:1563-1564)
+            r.s.visible_position = s.visible_position;
+            r.s.visible_normal = s.visible_normal;
+        }
+    }
+    r.count = r_count;
+    r.lifetime = r_lifetime;
+    r.w_sum = r_w_sum;
+    r.w2_sum = r_w2_sum;
     float m = (float)F.max_spatial_reuse_count;
     if (r.count > m) {
         r.w_sum *= m / r.count;
@@ -1027,13 +1121,13 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 }
 
 template <bool EMISSIVE_LIT, bool WINDOW>
-__global__ __launch_bounds__(256) HK_TRACE_OCC void k_spatial(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, ChannelArgs C)
 {
     __shared__ float win[WINDOW ? SP_WIN * SP_WIN : 1];
     DepthWin W{nullptr, 0, 0};
     if (WINDOW) {
         int32_t x0, y0;
-        tile_origin<HK_SPATIAL_ORDER>(A.F.s_row0, x0, y0);
+        tile_origin<HK_SPATIAL_ORDER>(A.F, A.F.s_row0, x0, y0);
         W.x0 = x0 - SP_HALO;
         W.y0 = y0 - SP_HALO;
         for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256)
@@ -1249,6 +1343,8 @@ __global__ __launch_bounds__(256) void k_trace(Scene sc, const float* rays, cons
 
 // ------------------------------------------------------------------ launchers
 static dim3 tiles(uint32_t width, int32_t rows) { return dim3((width + 15u) / 16u, ((uint32_t)rows + 15u) / 16u, 1); }
+// the tile grid of a launch: its window's rows (Frame::win_rows), else the plane's
+static dim3 tiles(const Frame& F, uint32_t width, int32_t rows) { return tiles(width, F.win_rows > 0 ? F.win_rows : rows); }
 
 // LDS staging is used when the kernel's scene arrays fit LDS_SCENE_MAX and the kernel gains from
 // it.  Measured on cornell 1080p (1 x MI355X): indirect 0.370 -> 0.317 ms; direct_lit even;
@@ -1270,7 +1366,7 @@ static uint32_t lds_plan_bytes(const FrameArgs& A, int plan, bool preferred)
 void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32_t stack_need, hipStream_t st)
 {
     const uint32_t lds = lds_plan_bytes(A, PLAN_GBUFFER, false);
-    const dim3 g = tiles(A.F.S[0], A.F.S_rows);
+    const dim3 g = tiles(A.F, A.F.S[0], A.F.S_rows);
     if (lds) hipLaunchKernelGGL((k_gbuffer<true, false>), g, dim3(256), lds, st, A, V, albedo);
     else if (stack_need <= (uint32_t)GB_STACK_LDS && !getenv("HK_GB_DEEP"))
         hipLaunchKernelGGL((k_gbuffer<false, true>), g, dim3(256), 0, st, A, V, albedo);
@@ -1278,7 +1374,7 @@ void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32
 }
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_albedo, tiles(A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, albedo);
+    hipLaunchKernelGGL(k_albedo, tiles(A.F, A.F.S[0], A.F.S_rows), dim3(256), 0, st, A, albedo);
 }
 // a validation frame of a direct-light pass: frame.number % interval == 0 (umod: interval 0 -> 0)
 static bool validation_frame(uint32_t number, uint32_t interval) { return interval == 0u || number % interval == 0u; }
@@ -1290,7 +1386,7 @@ static void launch_direct_v(const FrameArgs& A, const ChannelArgs& C, bool val, 
 }
 void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
 {
-    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
     if (emissive_lit) {
         const bool val = validation_frame(A.F.number, A.F.emissive_validate_interval);
@@ -1326,7 +1422,7 @@ static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const Chan
 }
 void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, hipStream_t st)
 {
-    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
     const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
     const bool ve = validation_frame(A.F.number, A.F.emissive_validate_interval);
@@ -1335,7 +1431,7 @@ void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const Channe
 }
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st)
 {
-    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, true);
     if (multi) {
         if (lds) hipLaunchKernelGGL((k_indirect<true, true>), g, dim3(256), lds, st, A, C);
@@ -1347,7 +1443,7 @@ void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipSt
 }
 void launch_indirect_wavefront(const FrameArgs& A, const ChannelArgs& C, const WfArgs& W, hipStream_t st)
 {
-    const dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    const dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, true);
     const dim3 per_seg(WF_SEGS * (W.seg_cap / 256u));      // every segment's entries, 256 per workgroup
     const dim3 all(((uint32_t)A.F.s[0] * (uint32_t)A.F.s_rows + 255u) / 256u);
@@ -1361,7 +1457,7 @@ void launch_indirect_wavefront(const FrameArgs& A, const ChannelArgs& C, const W
 }
 void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
 {
-    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     // the window assumes integrator pixels == deferred pixels (upscale ratio 1)
     const bool window = A.F.upscale_ratio == 1.0f && A.F.s[0] == A.F.S[0] && A.F.s[1] == A.F.S[1];
     if (emissive_lit) {
@@ -1374,7 +1470,7 @@ void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit,
 }
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
 {
-    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     if (D.channels == 3) hipLaunchKernelGGL(k_demod3<3>, g, dim3(256), 0, st, A, D);
     else hipLaunchKernelGGL(k_demod3<2>, g, dim3(256), 0, st, A, D);
 }
@@ -1390,13 +1486,13 @@ static void launch_level(const FrameArgs& A, const DenoiseArgs& D, int level, di
 }
 void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st)
 {
-    dim3 g = tiles(A.F.s[0], A.F.s_rows);
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     if (D.channels == 3) launch_level<3>(A, D, level, g, st);
     else launch_level<2>(A, D, level, g, st);
 }
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_tone, tiles(A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
+    hipLaunchKernelGGL(k_tone, tiles(A.F, A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
 }
 // ------------------------------------------------------------------ sub-frame accumulation
 __global__ __launch_bounds__(256) void k_accumulate(const uint2* tone, float4* acc, uint32_t n, int reset)

@@ -10,6 +10,7 @@
 // hk_denoise in PostProcessNode::run order (post_process.rs:1190-1224).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -497,6 +498,38 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.cnt.emitter = c->counters + COUNTER_SPAN;
     A.cnt.primary = c->counters + 2 * COUNTER_SPAN;
     return A;
+}
+
+// Per-pass launch windows of a row band (hk_resize with a halo).  A band recomputes halo rows so
+// that its own ("core") rows see exactly the inputs of a whole-frame render; each pass needs
+// fewer of them than the one before it, counted back from the tone-sum (core rows only):
+//   the a-trous levels L3..L0 read their input at +-1, 2, 4, 8 px (denoise.wgsl:101-114), so
+//   L3, L2, L1, L0 run on core +-0, 1, 3, 7 rows and demodulation on +-15; its 3x3 variance blur
+//   (denoise.wgsl:151-159) reads the light passes' render / variance at +-16 (OUT);
+//   spatial reuse runs on core +-OUT and reads the temporal reservoirs and the G-buffer depth
+//   within its RANGE (20 px indirect, 10 emissive: light.wgsl:1568-1600), so the temporal
+//   passes and the G-buffer run on core +-(OUT + RANGE).
+// For a static camera every other read is the pixel's own (temporal reprojection is the
+// identity), so the core rows stay bit-identical to the whole frame (test_gpu_row_bands_*),
+// with 1.15x instead of 1.30x the work of an 8-way city 4K band.  Rows outside a pass's window
+// keep stale values that no windowed pass reads.  HK_BAND_FULL_WINDOWS=1: every pass on all rows.
+constexpr int32_t DENOISE_OUT_REACH = 16, SPATIAL_RANGE = 20, EMISSIVE_SPATIAL_RANGE = 10;
+constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
+FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
+{
+    if (c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows) return A;
+    static const bool full = getenv("HK_BAND_FULL_WINDOWS") && getenv("HK_BAND_FULL_WINDOWS")[0] == '1';
+    if (full) return A;
+    const int32_t lo = std::max(0, c->core_row0 - margin);
+    const int32_t hi = std::min(c->s_rows, c->core_row0 + c->core_rows + margin);
+    A.F.win_row0 = lo;
+    A.F.win_rows = hi - lo;
+    return A;
+}
+int32_t light_out_reach(const hk_settings* st) { return st->denoise ? DENOISE_OUT_REACH : 0; }
+int32_t spatial_range(const hk_settings* st)
+{
+    return st->indirect_spatial_reuse ? SPATIAL_RANGE : (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0);
 }
 
 int check_ready(hk_ctx* c, bool need_scene)
@@ -1096,6 +1129,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     V.previous_models = c->prev_models;
     // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
     // hk_render_frame runs it on its own only for host-supplied G-buffers
+    A = pass_window(c, A, GBUFFER_REACH);
     timed(c, "gbuffer", gs, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, gs); });
     if (c->models_dirty) {  // this frame's models become the next frame's previous ones
         HK_HIP(c, hipMemcpy2DAsync(c->prev_models, 64, (const char*)c->buf[4] + offsetof(hk_instance, model),
@@ -1205,7 +1239,14 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         HK_HIP(c, hipEventRecord(c->ev_fork, st));
         HK_HIP(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
     }
-    if (!c->albedo_fresh) timed(c, "full_screen_albedo", st, [&] { launch_albedo(A, c->albedo, st); });
+    const FrameArgs A_all = A;
+    if (!c->albedo_fresh) {
+        const FrameArgs AG = pass_window(c, A_all, GBUFFER_REACH);
+        timed(c, "full_screen_albedo", st, [&] { launch_albedo(AG, c->albedo, st); });
+    }
+    // per-pass row windows of a band (pass_window): temporal passes, then spatial reuse
+    A = pass_window(c, A_all, light_out_reach(settings) + spatial_range(settings));
+    const FrameArgs AS = pass_window(c, A_all, light_out_reach(settings));
     ChannelArgs C0 = channel(c, A.F.number, 0);
     ChannelArgs C1 = channel(c, A.F.number, 1);
     // direct_lit + emissive in one launch when every reprojection is the identity: see
@@ -1225,7 +1266,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         timed(c, "direct_lit", st, [&] { launch_direct(A, C0, false, st); });
         timed(c, "direct_emissive", s1, [&] { launch_direct(A, C1, true, s1); });
     }
-    if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(A, C1, true, s1); });
+    if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(AS, C1, true, s1); });
     ChannelArgs C2 = channel(c, A.F.number, 2);
     bool multi = settings->indirect_bounces >= 2u;
     // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
@@ -1239,7 +1280,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     } else {
         timed(c, multi ? "indirect_multiple_bounces" : "indirect_lit_ambient", s2, [&] { launch_indirect(A, C2, multi, s2); });
     }
-    if (settings->indirect_spatial_reuse) timed(c, "indirect_spatial_reuse", s2, [&] { launch_spatial(A, C2, false, s2); });
+    if (settings->indirect_spatial_reuse) timed(c, "indirect_spatial_reuse", s2, [&] { launch_spatial(AS, C2, false, s2); });
     if (fork) {
         HK_HIP(c, hipEventRecord(c->ev_join[1], s2));
         HK_HIP(c, hipStreamWaitEvent(st, c->ev_join[1], 0));
@@ -1278,8 +1319,14 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     }
     D.geom = c->geom;
     c->last_denoised_channels = channels;
-    timed(c, "demodulation", st, [&] { launch_demod(A, D, st); });
-    for (int level = 0; level < 4; ++level) timed(c, "denoise", st, [&] { launch_denoise(A, D, level, st); });
+    // band windows (pass_window): demodulation on core +-15, the levels on +-7, 3, 1, 0
+    const FrameArgs AD = pass_window(c, A, DENOISE_OUT_REACH - 1);
+    timed(c, "demodulation", st, [&] { launch_demod(AD, D, st); });
+    static constexpr int32_t LEVEL_REACH[4] = {7, 3, 1, 0};
+    for (int level = 0; level < 4; ++level) {
+        const FrameArgs AL = pass_window(c, A, LEVEL_REACH[level]);
+        timed(c, "denoise", st, [&] { launch_denoise(AL, D, level, st); });
+    }
     if (async) HK_TRY(tail_end(c));
     HK_HIP(c, hipGetLastError());
     return HK_OK;
@@ -1298,7 +1345,7 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     else HK_TRY(gb_join(c, st));
     hk_frame_inputs dummy;
     std::memset(&dummy, 0, sizeof(dummy));
-    FrameArgs A = frame_args(c, settings, &dummy);
+    const FrameArgs A = pass_window(c, frame_args(c, settings, &dummy), 0);
     ToneArgs T;
     T.direct = settings->denoise ? c->denoised[0] : c->render[0];
     T.emissive = settings->denoise ? c->denoised[1] : c->render[1];

@@ -185,22 +185,27 @@ def test_trace_matches_oracle():
     assert (a[:, 3] != 0xFFFFFFFF).mean() > 0.5
 
 
-@pytest.mark.parametrize("spatial,denoise", [(True, True), (False, False)])
-def test_gpu_row_bands_match_whole_frame(spatial, denoise):
-    """Two band contexts (the multi-GPU decomposition, run on one GPU) reproduce the
-    whole-frame oracle render bit-exactly on their own rows, and count only their own rays."""
+@pytest.mark.parametrize("spatial,denoise,world,H", [(True, True, 2, 96), (False, False, 2, 96), (True, True, 4, 192),
+                                                     (True, False, 3, 192), (False, True, 3, 192)])
+def test_gpu_row_bands_match_whole_frame(spatial, denoise, world, H):
+    """Band contexts (the multi-GPU decomposition, run on one GPU) reproduce the whole-frame
+    oracle render bit-exactly on their own rows, and count only their own rays.  At H = 192 the
+    bands' halos and the per-pass row windows (hk_runtime.hip pass_window: G-buffer and temporal
+    passes on core +-36, spatial reuse +-16, demodulation +-15, the a-trous levels +-7/3/1/0) are
+    strict parts of the frame, over 5 frames of reservoir history."""
     from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
     from hikari_amd.bands import band_of, halo_rows
     from oracle import Oracle
-    W, H = 64, 96
+    W = 64
     scene, cam, lights = examples.cornell()
     desc = scene.build()
-    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=spatial, denoise=denoise)
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=spatial, emissive_spatial_reuse=spatial,
+                        denoise=denoise)
     s = st.to_c()
     o = Oracle(desc, load_noise(), W, H, 1.0)
     ranks = []
-    for k in range(2):
-        b = band_of(k, 2, H)
+    for k in range(world):
+        b = band_of(k, world, H)
         r = HikariRenderer(0)
         r.set_noise()
         r.upload_scene(scene)
