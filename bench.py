@@ -82,6 +82,10 @@ CONFIGS = {
     "city-4k-dynamic": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, dynamic=True,
                             workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, rotating "
                                      "emissive sphere: GPU instance/TLAS/light-BVH rebuild every frame"),
+    # configs[0]: the reference's CPU-runnable case (a parity case; bench line for completeness)
+    "cornell-256-all": dict(scene="cornell", width=256, height=256, spatial=True, denoise=True,
+                            workload="examples/cornell.rs 256x256 1spp, all passes (ReSTIR temporal/spatial "
+                                     "+ SVGF denoise)"),
     # per-frame fixed cost probe (launch / host overhead floor); not a BASELINE config
     "cornell-tiny-overhead": dict(scene="cornell", width=64, height=64, spatial=False, denoise=False,
                                   workload="examples/cornell.rs 64x64 (host/launch overhead probe)"),
