@@ -44,25 +44,36 @@ from hikari_amd.bands import band_of, halo_rows, stripe_gather_rows, use_stripes
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 # Compulsory HBM bytes per pixel per launch (reference texel formats; DESIGN.md "Roofline"):
+# Algorithmic HBM bytes per pixel of each kernel, (covered pixel, background pixel): the reference's
+# texel / record formats each kernel must read and write once.  A background pixel
+# (G-buffer depth 0) takes the passes' early exits: the temporal passes then store a zero reservoir
+# into three buffers (light.wgsl:1063-1071), spatial reuse copies the temporal record.
 BYTES_PER_PIXEL = {
-    "gbuffer": 60,                   # writes position 16 + normal 4 + gradient 8 + ids 8 + velocity/uv 16
+    "gbuffer": (60, 60),             # writes position 16 + normal 4 + gradient 8 + ids 8 + velocity/uv 16
                                      # + the fused full_screen_albedo's RGBA16F 8
-    "full_screen_albedo": 52,        # reads 44 B of G-buffer, writes RGBA16F
-    "direct_lit": 184,               # G 44 + reservoir read 64 + write 64 + variance 4 + render 8
-    "direct_emissive": 184,
-    "direct_lit_emissive": 324,      # both passes in one launch (k_direct_fused): the G-buffer read once,
-                                     # 2 x (reservoir read 64 + write 64 + variance 4 + render 8)
-    "indirect_lit_ambient": 184,
-    "indirect_multiple_bounces": 184,
-    "indirect_wavefront": 184,       # the same compulsory streams (queues / hit records are extra traffic)
-    "indirect_spatial_reuse": 244,   # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8
-    "emissive_spatial_reuse": 244,
-    "demodulation": 148,             # reads G-buffer normal 4 + position 16 (RGBA32F texel, .w used) + ids 8 +
+    "full_screen_albedo": (52, 52),  # reads 44 B of G-buffer, writes RGBA16F
+    # G 44 + reservoir read 64 + write 64 + variance 4 + render 8 | position 16 + 3 x 64 + 4 + 8; direct_lit's
+    # background pixels store only their temporal record (the emissive pass rewrites the shared spatial pair)
+    "direct_lit": (184, 92),
+    "direct_emissive": (184, 220),
+    "direct_lit_emissive": (324, 296),  # both passes in one launch (k_direct_fused): the G-buffer read once
+    "indirect_lit_ambient": (184, 220),
+    "indirect_multiple_bounces": (184, 220),
+    "indirect_wavefront": (184, 220),    # the same compulsory streams (queues / hit records are extra traffic)
+    # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8 | position 16 + 64 + 64 + 8
+    "indirect_spatial_reuse": (244, 152),
+    "emissive_spatial_reuse": (244, 152),
+    "demodulation": (148, 148),      # reads G-buffer normal 4 + position 16 (RGBA32F texel, .w used) + ids 8 +
                                      # depth gradient 8 + albedo 8 + 3 x (render 8 + variance 4); writes geom 32
                                      # (the levels' per-pixel geometry) + 3 x (internal 8 + ivar 4)
-    "denoise": 120,                  # geom 32 + 3 x (ivar 4 + input 8 + output 8) (+ albedo 8 at L3)
-    "tone_mapping": 32,
+    "denoise": (120, 56),            # geom 32 + 3 x (ivar 4 + input 8 + output 8) (+ albedo 8 at L3) | geom 32 + 3 x 8
+    "tone_mapping": (32, 32),
 }
+
+
+def kernel_bytes(name: str, covered_px: float, background_px: float) -> float:
+    c, b = BYTES_PER_PIXEL.get(name, (0, 0))
+    return c * covered_px + b * background_px
 
 CONFIGS = {
     # BASELINE.json configs[1]
@@ -332,6 +343,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timing = r.kernel_timing()
+    # fraction of the rank's pixels with geometry (G-buffer depth > 0): background pixels take the
+    # passes' early exits and move different bytes (BYTES_PER_PIXEL); read after the timed region
+    depth = r.output(11).view(np.float32).reshape(-1, 4)[:, 3]
+    coverage = float((depth >= np.finfo(np.float32).eps).mean())
     c = r.counters()
     rays = c["traverse_top"] + c["traverse_emitter"]
     primary = c["primary"]
@@ -397,8 +412,9 @@ def main():
             per_frame[name] = avg * launches
         dom = max(per_frame, key=per_frame.get)
         pix = W * rows
-        alg = BYTES_PER_PIXEL.get(dom, 0) * pix
-        frame_bytes = int(sum(BYTES_PER_PIXEL.get(k, 0) * {"denoise": 4}.get(k, 1) for k in timing) * pix * spp)
+        cov_px, bg_px = pix * coverage, pix * (1.0 - coverage)
+        alg = int(kernel_bytes(dom, cov_px, bg_px))
+        frame_bytes = int(sum(kernel_bytes(k, cov_px, bg_px) * {"denoise": 4}.get(k, 1) for k in timing) * spp)
         achieved = alg / (timing[dom] * 1e-3) / 1e9
         # the committed PMC numbers are per launch of a whole 1-GPU frame; a band launch differs
         traffic = load_pmc_traffic(args.config, dom) if world == 1 else None
@@ -426,7 +442,8 @@ def main():
                                        f"row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg, "avg_ms": round(timing[dom], 4),
+                         "algorithmic_bytes_per_launch": alg, "coverage": round(coverage, 4),
+                         "avg_ms": round(timing[dom], 4),
                          # all kernels of a frame together (they overlap: the indirect chain runs on a
                          # side stream next to direct/emissive, so per-kernel durations include sharing)
                          "frame_algorithmic_bytes": frame_bytes,

@@ -304,8 +304,14 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
         Reservoir r = zero_reservoir();
         set_reservoir(r, s, 0.0f);
         store_res(C.cur, idx, r);
-        store_res(C.spatial, idx, r);
-        store_res(C.prev_spatial, idx, r);
+        // direct_lit (light.wgsl:1063-1071) also stores this zero reservoir into the spatial pair,
+        // which it shares with the emissive pass (light.rs:518-546); the emissive pass, always run
+        // next in the frame, stores the same bits at the same two addresses after every direct_lit
+        // store of the frame, so the direct pass's two stores are dead and are skipped
+        if (EMISSIVE_LIT) {
+            store_res(C.spatial, idx, r);
+            store_res(C.prev_spatial, idx, r);
+        }
         C.variance[idx] = 0.0f;
         store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
         return;
@@ -346,7 +352,15 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
         if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
         if (trace) {
             n_top++;
+#ifdef HK_EXPERIMENT_NO_SHADOW  // timing experiment only (breaks parity): shadow rays never hit
+            Hit hit;
+            hit.uv = mk2(0, 0);
+            hit.distance = HK_F32_MAX;
+            hit.instance_index = HK_U32_MAX;
+            hit.primitive_index = HK_U32_MAX;
+#else
             Hit hit = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
+#endif
             occlude_hit_info(ray, hit, info);
             s.radiance = EMISSIVE_LIT ? input_radiance(sc, F, ray, info, false, cand.emissive_instance, false)
                                       : input_radiance(sc, F, ray, info, true, DONT_SAMPLE_EMISSIVE, false);

@@ -1,0 +1,15 @@
+#!/bin/bash
+# HBM traffic passes (FETCH_SIZE, WRITE_SIZE; one counter group per rocprofv3 run, kernel-trace only)
+# for the bench configs.  usage (GPU box): bash tools/pmc_traffic.sh <outdir> [configs...]
+set -e
+OUT=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $R/$OUT
+cd /tmp && export TMPDIR=/tmp
+for cfg in "$@"; do
+  for group in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $group --output-format csv -d $R/$OUT/$cfg/$group -o run -- \
+      python $R/bench.py --config $cfg --steps 8 --warmup 2 --cpu-budget 0 > $R/$OUT/$cfg.$group.log 2>&1
+    echo "$cfg $group ok"
+  done
+done
