@@ -141,6 +141,49 @@ def test_frame_pipelining_bit_exact(monkeypatch, denoise):
     assert r.counters() == o.counters()
 
 
+def test_device_pointer_after_sync_is_current(monkeypatch):
+    """The zero-copy route of INTEGRATION.md §3: with frame pipelining forced on, a reader that takes
+    hk_output_device_ptr and makes its own stream wait with hk_sync reads the frame's finished
+    planes (tone-mapped, denoised, G-buffer) — copied with hipMemcpyAsync on that stream, bit-equal
+    to the oracle's — without any other readback in between."""
+    import ctypes
+
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    monkeypatch.setenv("HK_PIPELINE_MIN_PX", "0")
+    # the HIP runtime libhikari_amd.so itself uses (torch may bring a second copy into the process)
+    maps = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln]
+    path = next((m for m in maps if m.startswith("/opt/rocm")), maps[0] if maps else "libamdhip64.so")
+    hip = ctypes.CDLL(path)
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    w, h = 96, 72
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=True)
+    scene, cam, lights, r, o = _setup(w, h, st)
+    s = st.to_c()
+    stream = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(stream)) == 0  # the reader's own stream
+    for f in range(6):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        r.sync(stream)
+        for oid in (10, 7, 8, 9, 11, 15):  # tone-mapped, denoised x3, G-buffer position, velocity
+            cw, ch, b = r.output_info(oid)
+            dst = np.empty((ch, cw, b), np.uint8)
+            ptr = r.output_device_ptr(oid)
+            assert ptr
+            assert hip.hipMemcpyAsync(dst.ctypes.data, ptr, dst.nbytes, 2, stream) == 0
+            assert hip.hipStreamSynchronize(stream) == 0
+            m = mismatch_report(canon_plane(oid, dst), canon_plane(oid, o.output(oid)), f"frame {f} output {oid}")
+            assert not m, m
+    hip.hipStreamDestroy(stream)
+
+
 def test_fallback_paths_bit_exact(monkeypatch):
     """The paths the defaults switch off stay exact: one stream (no channel fork), walk nodes
     without leaf collapse, the G-buffer stack with its scratch overflow levels."""
