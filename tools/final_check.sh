@@ -1,13 +1,19 @@
 #!/bin/bash
-# Round-end check on one GPU: the GPU parity suite, smoke(), the default bench line and a
-# 2-rank rehearsal of the multi-GPU bench path (both ranks on the one GPU, gloo collectives).
-# usage (on the GPU box): bash tools/final_check.sh
+# Round-end check on one GPU: the GPU parity suite, smoke(), the default bench line, its rocprofv3
+# kernel statistics and a 2-rank rehearsal of the multi-GPU bench path (both ranks on the one GPU,
+# gloo collectives).  usage (on the GPU box): bash tools/final_check.sh [tag]
 set -e
+TAG=${1:-final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_final2.log 2>&1
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_final2.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench_final2.json 2> gpurun_out/bench_final2.err
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+tail -1 $OUT/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+timeout -k 10 300 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+   -d $R/$OUT/stats -o run -- python $R/bench.py --steps 20 --warmup 3 --cpu-budget 0 > $R/$OUT/stats.log 2>&1)
 HK_BENCH_REHEARSAL=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/rehearsal3.log 2>&1
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 > $OUT/rehearsal.log 2>&1
+echo final-done
