@@ -203,11 +203,18 @@ struct GBuffer {
     float4* velocity_uv;
 };
 
-// SoA reservoir buffer: 4 planes of N 16-byte chunks.
+// Reservoir buffer of N 64-byte PackedReservoir records, as 16-byte chunks.  HK_RES_AOS = 0: SoA,
+// 4 planes of N chunks (chunk k of record i at k * N + i: a wave's 64 consecutive records are one
+// 1-KiB coalesced load per chunk); 1: the reference's AoS order (chunk k of record i at 4 i + k: a
+// gathered record is one 64-byte segment instead of four).
+#ifndef HK_RES_AOS
+#define HK_RES_AOS 0
+#endif
 struct ResBuf {
     uint4* base;
-    uint32_t n;  // records per plane
+    uint32_t n;  // records
 };
+__host__ __device__ __forceinline__ uint32_t res_chunk(const ResBuf& b, uint32_t k, uint32_t i) { return HK_RES_AOS ? 4u * i + k : k * b.n + i; }
 
 struct Counters {
     unsigned long long* top;
@@ -471,7 +478,8 @@ HKD Reservoir unpack_reservoir(uint4 c0, uint4 c1, uint4 c2, uint4 c3)
 HKD Reservoir load_res(const ResBuf& b, int32_t i)
 {
     const uint4* p = b.base;
-    return unpack_reservoir(p[i], p[b.n + i], p[2 * b.n + i], p[3 * b.n + i]);
+    const uint32_t u = (uint32_t)i;
+    return unpack_reservoir(p[res_chunk(b, 0, u)], p[res_chunk(b, 1, u)], p[res_chunk(b, 2, u)], p[res_chunk(b, 3, u)]);
 }
 HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
 {
@@ -489,10 +497,11 @@ HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
     c3.x = hk_pack4x8snorm(r.s.visible_normal.x, r.s.visible_normal.y, r.s.visible_normal.z, r.lifetime / 127.0f - 1.0f);
     c3.y = hk_pack4x8snorm(r.s.sample_normal.x, r.s.sample_normal.y, r.s.sample_normal.z, r.s.sample_position.w);
     uint4* p = b.base;
-    p[i] = c0;
-    p[b.n + i] = c1;
-    p[2 * b.n + i] = c2;
-    p[3 * b.n + i] = c3;
+    const uint32_t u = (uint32_t)i;
+    p[res_chunk(b, 0, u)] = c0;
+    p[res_chunk(b, 1, u)] = c1;
+    p[res_chunk(b, 2, u)] = c2;
+    p[res_chunk(b, 3, u)] = c3;
 }
 
 HKD void set_reservoir(Reservoir& r, const Sample& s, float w_new)

@@ -944,7 +944,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         sel = SEL_PREVIOUS;
         r_count = r_lifetime = r_w_sum = r_w2_sum = 0.0f;
         if (previous_index >= 0) {
-            const uint4 p3 = C.prev_spatial.base[3u * C.prev_spatial.n + (uint32_t)previous_index];
+            const uint4 p3 = C.prev_spatial.base[res_chunk(C.prev_spatial, 3u, (uint32_t)previous_index)];
             r_count = unpack_lo16float(p3.z);
             r_w_sum = unpack_lo16float(p3.w);
             r_w2_sum = unpack_hi16float(p3.w);
@@ -1006,12 +1006,12 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         // tests read plane 3 (count, normals) and plane 2 (sample position); planes 0-1 only for a
         // neighbour that is merged): the same values as load_res, fewer gathers for rejected ones
         const int32_t nidx = s_index(F, scx, scy);
-        const uint4 c3 = C.cur.base[3u * C.cur.n + (uint32_t)nidx];
+        const uint4 c3 = C.cur.base[res_chunk(C.cur, 3u, (uint32_t)nidx)];
         const float q_count = unpack_lo16float(c3.z);
         const f3 q_normal = normalize(mk3(hk_unpack_snorm8(c3.x, 0), hk_unpack_snorm8(c3.x, 1), hk_unpack_snorm8(c3.x, 2)));
         bool normal_miss = dot(s_normal, q_normal) < 0.866f;
         if (q_count < HK_F32_EPSILON || normal_miss) continue;
-        const uint4 c2 = C.cur.base[2u * C.cur.n + (uint32_t)nidx];
+        const uint4 c2 = C.cur.base[res_chunk(C.cur, 2u, (uint32_t)nidx)];
         const f3 q_sample = mk3(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z));
         // normalize(q_sample - visible), its length kept for the jacobian below
         const f3 to_sample = q_sample - s_visible;
@@ -1058,7 +1058,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         lane_stats_.tick();
 #endif
         // merge_reservoir(r, q, p / jacobian): the fields of q that the merge reads
-        const uint4 c0 = C.cur.base[(uint32_t)nidx];
+        const uint4 c0 = C.cur.base[res_chunk(C.cur, 0u, (uint32_t)nidx)];
         const float q_w = unpack_hi16float(c3.z);
         const f4 q_radiance = mk4(unpack_lo16float(c0.x), unpack_hi16float(c0.x), unpack_lo16float(c0.y),
                                   unpack_hi16float(c0.y));
@@ -1072,7 +1072,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             // compute_jacobian(q.s, s) (light.wgsl:990-1004).  Its first vector, visible - q_sample,
             // is -to_sample exactly, so its normalisation is -sample_direction and its length is
             // to_sample_length, bit for bit (negation is exact; the squares are equal)
-            const uint4 c1 = C.cur.base[C.cur.n + (uint32_t)nidx];
+            const uint4 c1 = C.cur.base[res_chunk(C.cur, 1u, (uint32_t)nidx)];
             const f3 q_visible = mk3(__uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z));
             const f3 normal = normalize(mk3(hk_unpack_snorm8(c3.y, 0), hk_unpack_snorm8(c3.y, 1), hk_unpack_snorm8(c3.y, 2)));
             const float c1_ = fabsf(dot(sample_direction, normal));
@@ -1096,16 +1096,14 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     // the selected sample, re-read from its record (see SEL_OWN above)
     Reservoir r;
     {
-        const uint4* base = C.cur.base;
-        uint32_t n = C.cur.n;
+        ResBuf b = C.cur;
         int32_t at = sel >= 0 ? sel : idx;
         if (sel == SEL_PREVIOUS) {
-            base = C.prev_spatial.base;
-            n = C.prev_spatial.n;
+            b = C.prev_spatial;
             at = previous_index;
         }
         if (at >= 0) {
-            r = unpack_reservoir(base[at], base[n + (uint32_t)at], base[2u * n + (uint32_t)at], base[3u * n + (uint32_t)at]);
+            r = load_res(b, at);
         } else {
             r = zero_reservoir();
         }

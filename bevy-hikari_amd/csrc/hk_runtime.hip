@@ -1575,9 +1575,10 @@ int hk_dump_reservoirs(hk_ctx* c, int id, hk_packed_reservoir* dst, size_t count
     std::vector<uint4> planes((size_t)4 * c->res_n);
     HK_HIP(c, hipMemcpyAsync(planes.data(), c->reservoirs[id], planes.size() * sizeof(uint4), hipMemcpyDeviceToHost, st));
     HK_HIP(c, hipStreamSynchronize(st));
+    const ResBuf layout{nullptr, c->res_n};
     for (size_t i = 0; i < count; ++i) {
         uint4* o = reinterpret_cast<uint4*>(dst + i);
-        for (int k = 0; k < 4; ++k) o[k] = planes[(size_t)k * c->res_n + i];
+        for (int k = 0; k < 4; ++k) o[k] = planes[res_chunk(layout, (uint32_t)k, (uint32_t)i)];
     }
     return HK_OK;
 }
@@ -1591,9 +1592,10 @@ int hk_load_reservoirs(hk_ctx* c, int id, const hk_packed_reservoir* src, size_t
     hipStream_t st = pick(c, stream);
     HK_TRY(gb_join(c, st));
     std::vector<uint4> planes((size_t)4 * c->res_n);
+    const ResBuf layout{nullptr, c->res_n};
     for (size_t i = 0; i < count; ++i) {
         const uint4* s = reinterpret_cast<const uint4*>(src + i);
-        for (int k = 0; k < 4; ++k) planes[(size_t)k * c->res_n + i] = s[k];
+        for (int k = 0; k < 4; ++k) planes[res_chunk(layout, (uint32_t)k, (uint32_t)i)] = s[k];
     }
     HK_HIP(c, hipMemcpyAsync(c->reservoirs[id], planes.data(), planes.size() * sizeof(uint4), hipMemcpyHostToDevice, st));
     HK_HIP(c, hipStreamSynchronize(st));
