@@ -288,15 +288,47 @@ __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
 // validate_interval != 0, light.wgsl:1096,1149), so the validation block is compiled out — it holds
 // the register peak (the reservoir stays live across its two walks: 142 -> 116 VGPRs for the emissive
 // pass, 3 -> 4 waves per SIMD) — and the candidate block always runs; 1 = the general body.
-template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true>
-HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top, uint32_t& n_emitter)
+// The G-buffer texels and the blue-noise sample a direct-light pass reads for its pixel
+// (light.wgsl:1052-1090).  Loaded once per thread: the fused launch runs both passes of the pixel
+// from one copy (the passes store only reservoir / render / variance planes, never the G-buffer),
+// where each pass loading its own would issue a second round of dependent loads after the first
+// pass's stores.  A background pixel (depth < epsilon) reads its position texel only.
+struct DirectPixel {
+    int32_t idx;
+    f2 uv;
+    f4 pd, velocity_uv, random;
+    f3 normal;
+    f2 imf;
+};
+HKD DirectPixel load_direct_pixel(const FrameArgs& A, int32_t x, int32_t y)
 {
     const Frame& F = A.F;
-    const int32_t idx = s_index(F, x, y);
-    const f2 uv = coords_to_uv(x, y, F.s);
+    DirectPixel p;
+    p.idx = s_index(F, x, y);
+    p.uv = coords_to_uv(x, y, F.s);
     int32_t dx, dy;
-    jittered_coords(F, uv, dx, dy);
-    f4 pd = load_position(F, A.G, dx, dy);
+    jittered_coords(F, p.uv, dx, dy);
+    p.pd = load_position(F, A.G, dx, dy);
+    p.normal = mk3(0, 0, 0);
+    p.imf = mk2(0, 0);
+    p.velocity_uv = p.random = mk4(0, 0, 0, 0);
+    if (p.pd.w >= HK_F32_EPSILON) {
+        p.normal = load_normal(F, A.G, dx, dy);
+        p.imf = load_instance_material(F, A.G, dx, dy);
+        p.velocity_uv = load_velocity_uv(F, A.G, dx, dy);
+        p.random = noise_random(A.noise, F.number, x, y);
+    }
+    return p;
+}
+
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true>
+HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel P, uint32_t& n_top,
+                     uint32_t& n_emitter)
+{
+    const Frame& F = A.F;
+    const int32_t idx = P.idx;
+    const f2 uv = P.uv;
+    f4 pd = P.pd;
     f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
     float depth = pd.w;
     Sample s = zero_sample();
@@ -316,12 +348,11 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
         store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
         return;
     }
-    f3 normal = load_normal(F, A.G, dx, dy);
-    f2 imf = load_instance_material(F, A.G, dx, dy);
-    uint32_t im_x = f2u32(imf.x), im_y = f2u32(imf.y);
-    f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
+    f3 normal = P.normal;
+    uint32_t im_x = f2u32(P.imf.x), im_y = f2u32(P.imf.y);
+    f4 velocity_uv = P.velocity_uv;
 
-    s.random = noise_random(A.noise, F.number, x, y);
+    s.random = P.random;
     s.visible_position = mk4(position.x, position.y, position.z, depth);
     s.visible_normal = normal;
     s.visible_instance = im_x;
@@ -431,7 +462,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_body<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
+        direct_body<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, load_direct_pixel(A, x, y), n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -454,7 +485,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_body<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
+        direct_body<false, true, VALIDATE>(A, sc, C, load_direct_pixel(A, x, y), n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -474,8 +505,9 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
-        direct_body<false, true, VD>(A, sc, C0, x, y, n_top, n_emitter);
-        direct_body<true, false, VE>(A, sc, C1, x, y, n_top, n_emitter);
+        const DirectPixel P = load_direct_pixel(A, x, y);
+        direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
+        direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -495,8 +527,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
-        direct_body<false, true, VD>(A, sc, C0, x, y, n_top, n_emitter);
-        direct_body<true, false, false>(A, sc, C1, x, y, n_top, n_emitter);
+        const DirectPixel P = load_direct_pixel(A, x, y);
+        direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
+        direct_body<true, false, false>(A, sc, C1, P, n_top, n_emitter);
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
