@@ -321,9 +321,73 @@ HKD DirectPixel load_direct_pixel(const FrameArgs& A, int32_t x, int32_t y)
     return p;
 }
 
-template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true>
+// Validation blocks park the reservoir in LDS across their walks (PARK): the block needs the
+// whole reservoir after the shadow walk (light.wgsl:1130-1150), and held in registers through
+// select_light_candidate's emitter walk and traverse_top it sets the kernel's register peak
+// (143-147 VGPRs, 3 waves per SIMD).  Each thread writes its 28 words to its own LDS column before
+// the walks and reads them back after; the compiler barriers keep the registers dead in between.
+#ifndef HK_VALIDATE_PARK
+#define HK_VALIDATE_PARK 1
+#endif
+constexpr int PARK_WORDS = 39;  // the reservoir (28) + the sample's radiance / sample point (11): 39 KiB per
+                                // workgroup, so 4 workgroups (4 waves per SIMD) fit a CU's 160 KiB
+#define HK_PARK_FIELDS(X)                                                                                                  \
+    X(0, s.radiance.x) X(1, s.radiance.y) X(2, s.radiance.z) X(3, s.radiance.w) X(4, s.random.x) X(5, s.random.y)         \
+    X(6, s.random.z) X(7, s.random.w) X(8, s.visible_position.x) X(9, s.visible_position.y) X(10, s.visible_position.z)   \
+    X(11, s.visible_position.w) X(12, s.visible_normal.x) X(13, s.visible_normal.y) X(14, s.visible_normal.z)             \
+    X(16, s.sample_position.x) X(17, s.sample_position.y) X(18, s.sample_position.z) X(19, s.sample_position.w)           \
+    X(20, s.sample_normal.x) X(21, s.sample_normal.y) X(22, s.sample_normal.z) X(23, count) X(24, lifetime) X(25, w)      \
+    X(26, w_sum) X(27, w2_sum)
+HKD void park_reservoir(float* lds, const Reservoir& r)
+{
+    const uint32_t t = threadIdx.x;
+#define HK_PARK_ST(k, f) lds[(k) * 256 + t] = r.f;
+    HK_PARK_FIELDS(HK_PARK_ST)
+#undef HK_PARK_ST
+    lds[15 * 256 + t] = __uint_as_float(r.s.visible_instance);
+    __asm__ volatile("" ::: "memory");
+}
+HKD Reservoir unpark_reservoir(const float* lds)
+{
+    const uint32_t t = threadIdx.x;
+    Reservoir r;
+#define HK_PARK_LD(k, f) r.f = lds[(k) * 256 + t];
+    HK_PARK_FIELDS(HK_PARK_LD)
+#undef HK_PARK_LD
+    r.s.visible_instance = __float_as_uint(lds[15 * 256 + t]);
+    return r;
+}
+HKD void park_sample(float* lds, const Sample& s)
+{
+    const uint32_t t = threadIdx.x;
+    const float v[11] = {s.radiance.x, s.radiance.y, s.radiance.z, s.radiance.w, s.sample_position.x, s.sample_position.y,
+                         s.sample_position.z, s.sample_position.w, s.sample_normal.x, s.sample_normal.y, s.sample_normal.z};
+#pragma unroll
+    for (int k = 0; k < 11; ++k) lds[(28 + k) * 256 + t] = v[k];
+    __asm__ volatile("" ::: "memory");
+}
+HKD void unpark_sample(const float* lds, Sample& s)
+{
+    const uint32_t t = threadIdx.x;
+    float v[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) v[k] = lds[(28 + k) * 256 + t];
+    s.radiance = mk4(v[0], v[1], v[2], v[3]);
+    s.sample_position = mk4(v[4], v[5], v[6], v[7]);
+    s.sample_normal = mk3(v[8], v[9], v[10]);
+}
+HKD float* park_area()
+{
+    __shared__ float park[PARK_WORDS * 256];
+    return park;
+}
+
+#ifndef HK_FUSED_SHARE_SURFACE
+#define HK_FUSED_SHARE_SURFACE 1
+#endif
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, bool PARK = false>
 HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel P, uint32_t& n_top,
-                     uint32_t& n_emitter)
+                     uint32_t& n_emitter, Surface* surface_out = nullptr, const Surface* surface_in = nullptr)
 {
     const Frame& F = A.F;
     const int32_t idx = P.idx;
@@ -403,20 +467,43 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     }
 
     if (VALIDATE && umod(F.number, validate_interval) == 0u) {
-        LightCandidate cand = select_light_candidate<true>(sc, F, r.s.random, xyz(r.s.visible_position),
-                                                           r.s.visible_normal, select_light_instance, info, n_emitter);
-        ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
-        ray.direction = normalize(xyz(r.s.sample_position) - xyz(s.visible_position));
-        ray.inv_direction = inv(ray.direction);
+        float* lds = nullptr;
+        if constexpr (PARK) {
+            lds = park_area();
+            park_sample(lds, s);
+            park_reservoir(lds, r);
+        }
+        LightCandidate cand;
+        {
+            const Reservoir rv = PARK ? unpark_reservoir(lds) : r;  // the fields the walks need
+            cand = select_light_candidate<true>(sc, F, rv.s.random, xyz(rv.s.visible_position), rv.s.visible_normal,
+                                                select_light_instance, info, n_emitter);
+            ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
+            ray.direction = normalize(xyz(rv.s.sample_position) - xyz(s.visible_position));
+            ray.inv_direction = inv(ray.direction);
+        }
+        // (r.s.visible_normal for the trace test below comes back with the reservoir)
         f4 validate_radiance = mk4(0, 0, 0, 0);
-        bool trace = dot(cand.direction, r.s.visible_normal) > 0.0f && cand.p > 0.0f;
+        bool trace;
+        if constexpr (PARK) {
+            const f3 vn = mk3(lds[12 * 256 + threadIdx.x], lds[13 * 256 + threadIdx.x], lds[14 * 256 + threadIdx.x]);
+            trace = dot(cand.direction, vn) > 0.0f && cand.p > 0.0f;
+        } else {
+            trace = dot(cand.direction, r.s.visible_normal) > 0.0f && cand.p > 0.0f;
+        }
         if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
+        if constexpr (PARK) __asm__ volatile("" ::: "memory");
         if (trace) {
             n_top++;
             Hit hit = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
             occlude_hit_info(ray, hit, info);
             validate_radiance = EMISSIVE_LIT ? input_radiance(sc, F, ray, info, false, cand.emissive_instance, false)
                                              : input_radiance(sc, F, ray, info, true, DONT_SAMPLE_EMISSIVE, false);
+        }
+        if constexpr (PARK) {
+            __asm__ volatile("" ::: "memory");
+            r = unpark_reservoir(lds);
+            unpark_sample(lds, s);
         }
         if (r.count >= 4.0f) {
             s.random = r.s.random;
@@ -444,7 +531,8 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     C.variance[idx] = variance_of(r);
     if (F.temporal_reuse > 0u) store_res(C.cur, idx, r);
 
-    Surface surface = retreive_surface(sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
+    Surface surface = surface_in ? *surface_in : retreive_surface(sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
+    if (surface_out) *surface_out = surface;
     f3 view_direction = calculate_view(F, position);
     f3 out = shading(F, view_direction, r.s.visible_normal, normalize(xyz(r.s.sample_position) - xyz(r.s.visible_position)),
                      surface, r.s.radiance);
@@ -506,8 +594,15 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
         const DirectPixel P = load_direct_pixel(A, x, y);
+#if HK_FUSED_SHARE_SURFACE
+        // the pixel's surface (same material and uv in both passes) is fetched once
+        Surface surface;
+        direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
+        direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
+#else
         direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
         direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
+#endif
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -517,7 +612,9 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
 // The fused launch on frames that are not emissive-validation frames, held to 4 waves per SIMD
 // (128 VGPRs): without the emissive validation block the body needs 117-137 VGPRs (the direct
 // validation block on every third frame), a few of which then spill.
-template <bool LDS, bool VD>
+// With the validation blocks parked in LDS (HK_VALIDATE_PARK, non-LDS-scene variants) the emissive
+// validation frames take this 4-wave kernel too (VE).
+template <bool LDS, bool VD, bool VE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_fused_w4(FrameArgs A, ChannelArgs C0,
                                                                                                    ChannelArgs C1)
 {
@@ -528,8 +625,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
         const DirectPixel P = load_direct_pixel(A, x, y);
+#if HK_FUSED_SHARE_SURFACE
+        // the pixel's surface (same material and uv in both passes) is fetched once
+        Surface surface;
+        direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
+        direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
+#else
         direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
-        direct_body<true, false, false>(A, sc, C1, P, n_top, n_emitter);
+        direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
+#endif
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -1458,7 +1562,10 @@ static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const Chan
                            uint32_t lds, hipStream_t st)
 {
     static const bool w4 = !getenv("HK_NO_FUSED_W4");
-    if (vd && ve) hipLaunchKernelGGL((k_direct_fused<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
+    if (HK_VALIDATE_PARK && !LDS && w4 && ve) {
+        if (vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
+        else hipLaunchKernelGGL((k_direct_fused_w4<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
+    } else if (vd && ve) hipLaunchKernelGGL((k_direct_fused<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
     else if (ve) hipLaunchKernelGGL((k_direct_fused<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
     else if (w4 && vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true>), g, dim3(256), lds, st, A, C0, C1);
     else if (w4) hipLaunchKernelGGL((k_direct_fused_w4<LDS, false>), g, dim3(256), lds, st, A, C0, C1);
