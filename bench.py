@@ -71,8 +71,21 @@ BYTES_PER_PIXEL = {
 }
 
 
-def kernel_bytes(name: str, covered_px: float, background_px: float) -> float:
+# Background store elision (hk_kernels.hip bg_elide): in steady state a background pixel of the
+# fused direct/emissive launch and of the indirect pass reads its position texel (16) and its mask
+# byte (1) and stores nothing — its targets already hold the constant zero words — except, when the
+# channel's spatial reuse runs (it rewrites the pair with other bits), both spatial-pair records
+# (2 x 64).  Not on with HK_NO_BG_ELIDE=1.
+BG_ELIDED_BYTES = {"direct_lit_emissive": ("emissive_spatial_reuse", 17, 145),
+                   "indirect_lit_ambient": ("indirect_spatial_reuse", 17, 145),
+                   "indirect_multiple_bounces": ("indirect_spatial_reuse", 17, 145)}
+
+
+def kernel_bytes(name: str, covered_px: float, background_px: float, settings=None) -> float:
     c, b = BYTES_PER_PIXEL.get(name, (0, 0))
+    if settings is not None and name in BG_ELIDED_BYTES and os.environ.get("HK_NO_BG_ELIDE") != "1":
+        flag, alone, with_pair = BG_ELIDED_BYTES[name]
+        b = with_pair if getattr(settings, flag) else alone
     return c * covered_px + b * background_px
 
 CONFIGS = {
@@ -413,8 +426,8 @@ def main():
         dom = max(per_frame, key=per_frame.get)
         pix = W * rows
         cov_px, bg_px = pix * coverage, pix * (1.0 - coverage)
-        alg = int(kernel_bytes(dom, cov_px, bg_px))
-        frame_bytes = int(sum(kernel_bytes(k, cov_px, bg_px) * {"denoise": 4}.get(k, 1) for k in timing) * spp)
+        alg = int(kernel_bytes(dom, cov_px, bg_px, st))
+        frame_bytes = int(sum(kernel_bytes(k, cov_px, bg_px, st) * {"denoise": 4}.get(k, 1) for k in timing) * spp)
         achieved = alg / (timing[dom] * 1e-3) / 1e9
         # the committed PMC numbers are per launch of a whole 1-GPU frame; a band launch differs
         traffic = load_pmc_traffic(args.config, dom) if world == 1 else None

@@ -541,6 +541,40 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     store_rgba16f(C.render, idx, mk4(out.x, out.y, out.z, 1.0f));
 }
 
+// Background store elision (ChannelArgs::bg).  A background pixel (G-buffer depth 0, or every
+// pixel of an indirect pass with no bounces) stores the same constant words on every frame: the
+// zero reservoir into the pass's temporal buffer and both spatial buffers, variance 0 and a zero
+// render texel (light.wgsl:1063-1071, 1283-1290).  The mask byte says which physical targets got
+// those words on an earlier frame and have not been written since; targets that all have are not
+// stored again — every buffer still ends the frame with the reference's bits.  A covered pixel
+// writes other values, so it clears its byte.  When the channel's spatial reuse runs, it rewrites
+// the spatial buffer with a repacked copy of the temporal record (light.wgsl:1566-1574: other
+// bits for the zero normal), so the pair alternates between two words and is stored every frame
+// (bg_need without BG_PAIR).  The runtime resets the mask whenever anything else may have written
+// these targets (a launch without the mask, reservoir uploads, reallocation, another pass window).
+enum BgElide : uint32_t { BG_STORE = 0, BG_SKIP_OWN = 1, BG_SKIP_ALL = 2 };
+constexpr uint32_t BG_PAIR = 16u;
+HKD uint32_t bg_elide(const ChannelArgs& C, int32_t idx, bool background)
+{
+    if (!C.bg) return BG_STORE;
+    const uint32_t m = C.bg[idx];
+    if (!background) {
+        if (m) C.bg[idx] = 0;
+        return BG_STORE;
+    }
+    const uint32_t own = C.bg_need & 15u, pair = C.bg_need & BG_PAIR;
+    const uint32_t nm = (m & 15u) | own | pair;
+    if (nm != m) C.bg[idx] = (uint8_t)nm;
+    if ((m & own) != own) return BG_STORE;
+    return (pair && (m & BG_PAIR)) ? BG_SKIP_ALL : BG_SKIP_OWN;
+}
+HKD Reservoir background_reservoir()
+{
+    Reservoir r = zero_reservoir();
+    set_reservoir(r, zero_sample(), 0.0f);
+    return r;
+}
+
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, ChannelArgs C)
 {
@@ -594,15 +628,22 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
         const DirectPixel P = load_direct_pixel(A, x, y);
+        const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
+        if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
+            const Reservoir z = background_reservoir();
+            store_res(C1.spatial, P.idx, z);
+            store_res(C1.prev_spatial, P.idx, z);
+        } else if (bg == BG_STORE) {
 #if HK_FUSED_SHARE_SURFACE
-        // the pixel's surface (same material and uv in both passes) is fetched once
-        Surface surface;
-        direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
-        direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
+            // the pixel's surface (same material and uv in both passes) is fetched once
+            Surface surface;
+            direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
+            direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
 #else
-        direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
-        direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
+            direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
+            direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
 #endif
+        }
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -625,15 +666,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
         const DirectPixel P = load_direct_pixel(A, x, y);
+        const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
+        if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
+            const Reservoir z = background_reservoir();
+            store_res(C1.spatial, P.idx, z);
+            store_res(C1.prev_spatial, P.idx, z);
+        } else if (bg == BG_STORE) {
 #if HK_FUSED_SHARE_SURFACE
-        // the pixel's surface (same material and uv in both passes) is fetched once
-        Surface surface;
-        direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
-        direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
+            // the pixel's surface (same material and uv in both passes) is fetched once
+            Surface surface;
+            direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
+            direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
 #else
-        direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
-        direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
+            direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
+            direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
 #endif
+        }
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -678,13 +726,20 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
     float depth = pd.w;
     Sample s = zero_sample();
     Reservoir r = zero_reservoir();
-    if (F.indirect_bounces == 0u || depth < HK_F32_EPSILON) {
+    const bool background = F.indirect_bounces == 0u || depth < HK_F32_EPSILON;
+    uint32_t bg = BG_STORE;
+    if constexpr (STAGE == IND_ALL) bg = bg_elide(C, idx, background);
+    if (background) {
         if constexpr (STAGE == IND_ALL || STAGE == IND_GEN) {
-            store_res(C.cur, idx, r);
-            store_res(C.spatial, idx, r);
-            store_res(C.prev_spatial, idx, r);
-            C.variance[idx] = 0.0f;
-            store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
+            if (bg != BG_SKIP_ALL) {
+                store_res(C.spatial, idx, r);
+                store_res(C.prev_spatial, idx, r);
+            }
+            if (bg == BG_STORE) {
+                store_res(C.cur, idx, r);
+                C.variance[idx] = 0.0f;
+                store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
+            }
         }
         return false;
     }

@@ -26,6 +26,13 @@ struct ChannelArgs {
     ResBuf spatial;       // spatial_reservoir_buffer
     float* variance;
     uint2* render;
+    // Background store elision (k_direct_fused / k_indirect only; nullptr elsewhere): one byte per
+    // pixel recording which of the pass's physical targets already hold a background pixel's
+    // constant zero words (bit r = reservoir parity r's temporal buffers, bit 2 + s = render /
+    // variance slot s, bit 4 = both buffers of the spatial pair).  bg_need = the bits this frame's
+    // stores target; when all are set the stores are skipped (same bits in every buffer).
+    uint8_t* bg;
+    uint32_t bg_need;
 };
 
 // Wavefront indirect pass (config 5: material-sorted shading), see hk_kernels.hip k_wf_*.

@@ -122,6 +122,11 @@ struct hk_ctx {
     uint2* render[3] = {};
     uint4* reservoirs[HK_RESERVOIR_BUFFERS] = {};
     uint32_t res_n = 0;
+    // background store elision masks (ChannelArgs::bg): [0] the fused direct/emissive pair, [1] the
+    // indirect channel; valid = the mask describes the buffers' contents for pass window key
+    uint8_t* bgmask[2] = {};
+    bool bg_valid[2] = {false, false};
+    int32_t bg_key[2][2] = {};
     // denoise
     uint2* internal[3][4] = {};
     float* internal_variance[3] = {};
@@ -269,6 +274,10 @@ void free_targets(hk_ctx* c)
         release(c->denoised[i]);
     }
     for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) release(c->reservoirs[i]);
+    for (int k = 0; k < 2; ++k) {
+        release(c->bgmask[k]);
+        c->bg_valid[k] = false;
+    }
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) release(c->internal[ch][i]);
         release(c->internal_variance[ch]);
@@ -1025,6 +1034,10 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
         HK_HIP(c, hipMalloc(&c->reservoirs[i], 4 * sp * sizeof(uint4)));
         HK_HIP(c, hipMemset(c->reservoirs[i], 0, 4 * sp * sizeof(uint4)));  // light.rs:355-358 zero-fill
     }
+    for (int k = 0; k < 2; ++k) {
+        HK_HIP(c, hipMalloc(&c->bgmask[k], sp));
+        c->bg_valid[k] = false;
+    }
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) {
             HK_HIP(c, hipMalloc(&c->internal[ch][i], sp * sizeof(uint2)));
@@ -1048,6 +1061,7 @@ int hk_set_band_halo(hk_ctx* c, uint32_t rows)
 {
     if (!c || rows > 4096) return HK_ERR_INVALID;
     c->halo = (int32_t)rows;
+    c->bg_valid[0] = c->bg_valid[1] = false;
     return HK_OK;
 }
 
@@ -1186,6 +1200,8 @@ static ChannelArgs channel(hk_ctx* c, uint32_t number, int ch)
     static const int pairs[3][2] = {{0, 4}, {2, 4}, {6, 8}};
     uint32_t current = number % 2u, previous = 1u - current;
     ChannelArgs C;
+    C.bg = nullptr;
+    C.bg_need = 0;
     C.prev = ResBuf{c->reservoirs[current + pairs[ch][0]], c->res_n};
     C.cur = ResBuf{c->reservoirs[previous + pairs[ch][0]], c->res_n};
     C.prev_spatial = ResBuf{c->reservoirs[current + pairs[ch][1]], c->res_n};
@@ -1193,6 +1209,31 @@ static ChannelArgs channel(hk_ctx* c, uint32_t number, int ch)
     C.variance = c->variance[ch];
     C.render = c->render[ch];
     return C;
+}
+
+// The background elision mask k (0: direct/emissive pair, 1: indirect) for a launch over window A
+// of this frame, or nullptr when the launch does not use it (use = false: another kernel writes the
+// channel's targets this frame, so the mask is dropped and rebuilt from zero the next time).
+static int bg_mask(hk_ctx* c, int k, const FrameArgs& A, bool use, bool pair, hipStream_t st, ChannelArgs& C)
+{
+    static const bool off = getenv("HK_NO_BG_ELIDE") && getenv("HK_NO_BG_ELIDE")[0] == '1';
+    C.bg = nullptr;
+    C.bg_need = 0;
+    if (!use || off) {
+        c->bg_valid[k] = false;
+        return HK_OK;
+    }
+    if (!c->bg_valid[k] || c->bg_key[k][0] != A.F.win_row0 || c->bg_key[k][1] != A.F.win_rows) {
+        HK_HIP(c, hipMemsetAsync(c->bgmask[k], 0, c->res_n, st));
+        c->bg_valid[k] = true;
+        c->bg_key[k][0] = A.F.win_row0;
+        c->bg_key[k][1] = A.F.win_rows;
+    }
+    C.bg = c->bgmask[k];
+    // targets of this frame: reservoir parity (the temporal buffer), render / variance slot, and
+    // (pair: no spatial reuse pass rewrites it) the spatial pair, both of whose buffers are stored
+    C.bg_need = (1u << (A.F.number & 1u)) | (4u << c->rslot) | (pair ? 16u : 0u);
+    return HK_OK;
 }
 
 int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in, void* stream)
@@ -1260,6 +1301,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     const double fuse_min_px = fmin ? atof(fmin) : (double)(1u << 20);
     const bool fuse = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f &&
                       (double)c->s[0] * (double)c->s_rows >= fuse_min_px && !getenv("HK_NO_FUSE");
+    HK_TRY(bg_mask(c, 0, A, fuse, !settings->emissive_spatial_reuse, st, C0));
     if (fuse) {
         timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(A, C0, C1, st); });
     } else {
@@ -1271,6 +1313,10 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     bool multi = settings->indirect_bounces >= 2u;
     // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
     const bool wf = c->wavefront && !multi && c->count[6] + 1u <= WF_MAX_BINS;
+    // (the indirect pass scatters rejected history to the reprojected pixel: elision only under the
+    // identity reprojection, where every store lands on the thread's own pixel)
+    const bool identity = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f;
+    HK_TRY(bg_mask(c, 1, A, !wf && identity, !settings->indirect_spatial_reuse, s2, C2));
     if (wf) {
         HK_TRY(ensure_wavefront(c));
         WfArgs W{c->wf_queue1, c->wf_keys, c->wf_queue2, c->wf_hit, c->wf_hit_t, c->wf_ctl, c->count[6] + 1u,
@@ -1598,6 +1644,7 @@ int hk_load_reservoirs(hk_ctx* c, int id, const hk_packed_reservoir* src, size_t
         for (int k = 0; k < 4; ++k) planes[res_chunk(layout, (uint32_t)k, (uint32_t)i)] = s[k];
     }
     HK_HIP(c, hipMemcpyAsync(c->reservoirs[id], planes.data(), planes.size() * sizeof(uint4), hipMemcpyHostToDevice, st));
+    c->bg_valid[0] = c->bg_valid[1] = false;  // the elision masks no longer describe the buffers
     HK_HIP(c, hipStreamSynchronize(st));
     return HK_OK;
 }
