@@ -75,8 +75,9 @@ BYTES_PER_PIXEL = {
 # fused direct/emissive launch and of the indirect pass reads its position texel (16) and its mask
 # byte (1) and stores nothing — its targets already hold the constant zero words — except, when the
 # channel's spatial reuse runs (it rewrites the pair with other bits), both spatial-pair records
-# (2 x 64).  Not on with HK_NO_BG_ELIDE=1.
-BG_ELIDED_BYTES = {"direct_lit_emissive": ("emissive_spatial_reuse", 17, 145),
+# (2 x 64); a G-buffer miss reads its mask byte only.  Not on with HK_NO_BG_ELIDE=1.
+BG_ELIDED_BYTES = {"gbuffer": (None, 1, 1),  # a miss: its mask byte (the slot already holds the zero texels)
+                   "direct_lit_emissive": ("emissive_spatial_reuse", 17, 145),
                    "indirect_lit_ambient": ("indirect_spatial_reuse", 17, 145),
                    "indirect_multiple_bounces": ("indirect_spatial_reuse", 17, 145)}
 
@@ -85,7 +86,7 @@ def kernel_bytes(name: str, covered_px: float, background_px: float, settings=No
     c, b = BYTES_PER_PIXEL.get(name, (0, 0))
     if settings is not None and name in BG_ELIDED_BYTES and os.environ.get("HK_NO_BG_ELIDE") != "1":
         flag, alone, with_pair = BG_ELIDED_BYTES[name]
-        b = with_pair if getattr(settings, flag) else alone
+        b = with_pair if flag and getattr(settings, flag) else alone
     return c * covered_px + b * background_px
 
 CONFIGS = {
@@ -463,6 +464,8 @@ def main():
                          "frame_achieved": round(frame_bytes / (ms * 1e-3) / 1e9, 1),
                          "frame_frac": round(frame_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
+            # each kernel alone on the GPU (the untimed isolated frames after the timed region)
+            "isolated_kernel_ms": None if not isolated else {k: round(v, 4) for k, v in isolated.items()},
         }
         if isolated and dom in isolated:
             # the same kernel with the GPU to itself (8 untimed frames after the timed region)

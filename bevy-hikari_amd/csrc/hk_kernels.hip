@@ -221,13 +221,23 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
         ray.inv_direction = inv(ray.direction);
         Hit hit = closest_hit_ordered<SHALLOW && !LDS>(sc, ray, LDS ? nullptr : gb_lds_stack);
         if (hit.instance_index == HK_U32_MAX) {
-            A.G.position[idx] = make_float4(0, 0, 0, 0);
-            A.G.normal[idx] = 0u;
-            A.G.depth_gradient[idx] = make_float2(0, 0);
-            A.G.instance_material[idx] = make_float2(0, 0);
-            A.G.velocity_uv[idx] = make_float4(0, 0, 0, 0);
-            if (albedo) store_rgba16f(albedo, idx, mk4(0, 0, 0, 0));
+            // a miss stores constant zeros: skipped when this slot already holds them (V.bg)
+            bool stored = false;
+            if (V.bg) {
+                const uint32_t m = V.bg[idx];
+                stored = (m & V.bg_need) != 0u;
+                if (!stored) V.bg[idx] = (uint8_t)(m | V.bg_need);
+            }
+            if (!stored) {
+                A.G.position[idx] = make_float4(0, 0, 0, 0);
+                A.G.normal[idx] = 0u;
+                A.G.depth_gradient[idx] = make_float2(0, 0);
+                A.G.instance_material[idx] = make_float2(0, 0);
+                A.G.velocity_uv[idx] = make_float4(0, 0, 0, 0);
+                if (albedo) store_rgba16f(albedo, idx, mk4(0, 0, 0, 0));
+            }
         } else {
+            if (V.bg && V.bg[idx]) V.bg[idx] = 0;
             HitInfo info = hit_info(sc, ray, hit);
             f3 p = xyz(info.position);
             float depth = ndc_depth(V.view_proj, p);

@@ -67,6 +67,10 @@ struct ViewArgs {
     int motion;
     float previous_view_proj[16];
     const float* previous_models;  // 16 floats per instance: model at the previous k_gbuffer
+    // background store elision (as ChannelArgs::bg): bit s = G-buffer slot s holds a miss pixel's
+    // zero texels in every plane (position, normal, gradient, ids, velocity/uv, albedo); nullptr = off
+    uint8_t* bg;
+    uint32_t bg_need;
 };
 
 // All channels of one frame (post_process.rs:1199-1223 runs them one after another).

@@ -127,6 +127,9 @@ struct hk_ctx {
     uint8_t* bgmask[2] = {};
     bool bg_valid[2] = {false, false};
     int32_t bg_key[2][2] = {};
+    uint8_t* gbmask = nullptr;  // the G-buffer's (ViewArgs::bg), per S pixel
+    bool gb_valid = false;
+    int32_t gb_key[2] = {};
     // denoise
     uint2* internal[3][4] = {};
     float* internal_variance[3] = {};
@@ -278,6 +281,8 @@ void free_targets(hk_ctx* c)
         release(c->bgmask[k]);
         c->bg_valid[k] = false;
     }
+    release(c->gbmask);
+    c->gb_valid = false;
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) release(c->internal[ch][i]);
         release(c->internal_variance[ch]);
@@ -1038,6 +1043,8 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
         HK_HIP(c, hipMalloc(&c->bgmask[k], sp));
         c->bg_valid[k] = false;
     }
+    HK_HIP(c, hipMalloc(&c->gbmask, SP));
+    c->gb_valid = false;
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) {
             HK_HIP(c, hipMalloc(&c->internal[ch][i], sp * sizeof(uint2)));
@@ -1144,6 +1151,18 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
     // hk_render_frame runs it on its own only for host-supplied G-buffers
     A = pass_window(c, A, GBUFFER_REACH);
+    V.bg = nullptr;
+    V.bg_need = 0;
+    if (!(getenv("HK_NO_BG_ELIDE") && getenv("HK_NO_BG_ELIDE")[0] == '1')) {
+        if (!c->gb_valid || c->gb_key[0] != A.F.win_row0 || c->gb_key[1] != A.F.win_rows) {
+            HK_HIP(c, hipMemsetAsync(c->gbmask, 0, (size_t)c->S[0] * c->S_rows, gs));
+            c->gb_valid = true;
+            c->gb_key[0] = A.F.win_row0;
+            c->gb_key[1] = A.F.win_rows;
+        }
+        V.bg = c->gbmask;
+        V.bg_need = 1u << c->gslot;  // the planes' physical slot (swapped with gslot above)
+    }
     timed(c, "gbuffer", gs, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, gs); });
     if (c->models_dirty) {  // this frame's models become the next frame's previous ones
         HK_HIP(c, hipMemcpy2DAsync(c->prev_models, 64, (const char*)c->buf[4] + offsetof(hk_instance, model),
@@ -1177,6 +1196,7 @@ int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, i
     default: return fail(c, HK_ERR_INVALID, "unknown G-buffer plane");
     }
     if (bytes != need) return fail(c, HK_ERR_INVALID, "G-buffer plane size mismatch");
+    c->gb_valid = false;  // host planes: the G-buffer elision mask no longer describes the slots
     // a new frame's position / velocity plane: the current one becomes the previous (prepass.rs:309-317)
     if (plane == 0) {
         std::swap(c->g_position, c->g_prev_position);

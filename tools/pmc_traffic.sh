@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 for cfg in "$@"; do
   for group in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $group --output-format csv -d $R/$OUT/$cfg/$group -o run -- \
-      python $R/bench.py --config $cfg --steps 8 --warmup 2 --cpu-budget 0 > $R/$OUT/$cfg.$group.log 2>&1
+      python $R/bench.py --config $cfg --steps ${PMC_STEPS:-8} --warmup 2 --cpu-budget 0 > $R/$OUT/$cfg.$group.log 2>&1
     echo "$cfg $group ok"
   done
 done
