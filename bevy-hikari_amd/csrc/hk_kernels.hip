@@ -585,6 +585,31 @@ HKD Reservoir background_reservoir()
     return r;
 }
 
+// The separate direct_lit / emissive launches share the pair's mask (ChannelArgs::bg of both):
+// direct_lit, first on the stream, only reads it (its targets are among the bits); the emissive
+// pass, which stores after it into the spatial pair, updates it for both.  Both classify a pixel
+// from the same G-buffer texel, so they agree on which pixels are background.
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE>
+HKD void direct_pass(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
+                     uint32_t& n_emitter)
+{
+    const DirectPixel P = load_direct_pixel(A, x, y);
+    const bool background = P.pd.w < HK_F32_EPSILON;
+    if constexpr (!EMISSIVE_LIT) {
+        if (C.bg && background && (C.bg[P.idx] & (C.bg_need & 15u)) == (C.bg_need & 15u)) return;
+    } else {
+        const uint32_t bg = bg_elide(C, P.idx, background);
+        if (bg == BG_SKIP_ALL) return;
+        if (bg == BG_SKIP_OWN) {
+            const Reservoir z = background_reservoir();
+            store_res(C.spatial, P.idx, z);
+            store_res(C.prev_spatial, P.idx, z);
+            return;
+        }
+    }
+    direct_body<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, P, n_top, n_emitter);
+}
+
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, ChannelArgs C)
 {
@@ -594,7 +619,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_body<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, load_direct_pixel(A, x, y), n_top, n_emitter);
+        direct_pass<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -617,7 +642,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_body<false, true, VALIDATE>(A, sc, C, load_direct_pixel(A, x, y), n_top, n_emitter);
+        direct_pass<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);

@@ -1321,7 +1321,12 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     const double fuse_min_px = fmin ? atof(fmin) : (double)(1u << 20);
     const bool fuse = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f &&
                       (double)c->s[0] * (double)c->s_rows >= fuse_min_px && !getenv("HK_NO_FUSE");
-    HK_TRY(bg_mask(c, 0, A, fuse, !settings->emissive_spatial_reuse, st, C0));
+    // background elision under the identity reprojection (every store on the thread's own pixel);
+    // the separate launches share the pair's mask (direct_pass)
+    const bool identity = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f;
+    HK_TRY(bg_mask(c, 0, A, identity, !settings->emissive_spatial_reuse, st, C0));
+    C1.bg = C0.bg;
+    C1.bg_need = C0.bg_need;
     if (fuse) {
         timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(A, C0, C1, st); });
     } else {
@@ -1333,9 +1338,6 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     bool multi = settings->indirect_bounces >= 2u;
     // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
     const bool wf = c->wavefront && !multi && c->count[6] + 1u <= WF_MAX_BINS;
-    // (the indirect pass scatters rejected history to the reprojected pixel: elision only under the
-    // identity reprojection, where every store lands on the thread's own pixel)
-    const bool identity = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f;
     HK_TRY(bg_mask(c, 1, A, !wf && identity, !settings->indirect_spatial_reuse, s2, C2));
     if (wf) {
         HK_TRY(ensure_wavefront(c));

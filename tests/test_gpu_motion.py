@@ -286,16 +286,21 @@ def test_forced_kernel_variants_bit_exact(monkeypatch, lds):
             monkeypatch.delenv(k)
 
 
-def test_background_elision_bit_exact(monkeypatch):
-    """Background store elision (ChannelArgs::bg, hk_kernels.hip bg_elided): the fused direct /
-    emissive launch and the indirect pass skip a background pixel's constant zero stores once
+@pytest.mark.parametrize("launch", ["fused", "separate"])
+def test_background_elision_bit_exact(monkeypatch, launch):
+    """Background store elision (ChannelArgs::bg, hk_kernels.hip bg_elide): the direct / emissive
+    launches (fused, or separate sharing one mask) and the indirect pass skip a background pixel's constant zero stores once
     every target buffer holds them.  A sequence that exercises every way the mask can go stale:
     static frames (elision active from the third frame), camera motion (separate launches: the
     mask is dropped), static again (rebuilt), and a reservoir upload over the spatial pairs,
     after which the next frame must store the background records again.  Every plane and all 10
     reservoir buffers bit-exact against the oracle (which never elides) on every frame."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
-    monkeypatch.setenv("HK_FUSE_MIN_PX", "0")
+    if launch == "fused":
+        monkeypatch.setenv("HK_FUSE_MIN_PX", "0")
+    else:  # direct_lit and the emissive pass as two launches sharing the mask (k_direct_lit_w4 too)
+        monkeypatch.setenv("HK_NO_FUSE", "1")
+        monkeypatch.setenv("HK_DIRECT_W4_MIN_PX", "0")
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=False, denoise=True)
     scene, cam, lights, r, o = _pair("cornell", w, h, st)
