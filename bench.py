@@ -473,6 +473,12 @@ def main():
             result["roofline"]["isolated_avg_ms"] = round(iso, 4)
             result["roofline"]["isolated_achieved"] = round(alg / (iso * 1e-3) / 1e9, 1)
             result["roofline"]["isolated_frac"] = round(alg / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            # the bytes the reference moves for the same launch (no background store elision: every
+            # background pixel stores its zero reservoirs / texels again), over the same time
+            ref = kernel_bytes(dom, cov_px, bg_px)
+            if ref != alg:
+                result["roofline"]["reference_format_bytes_per_launch"] = int(ref)
+                result["roofline"]["isolated_reference_format_frac"] = round(ref / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         tb = load_traversal_bytes(args.config) if world == 1 and spp == 1 else None
         if tb is not None:
             # §8d's second component: node / triangle / instance / hit_info bytes of the light passes

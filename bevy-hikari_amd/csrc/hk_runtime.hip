@@ -115,6 +115,7 @@ struct hk_ctx {
     uint32_t head = 0;                    // frame_number % 2 (PostProcessTextures.head)
     // channel fork-join: emissive and indirect passes on side streams next to direct_lit
     hipStream_t side[2] = {nullptr, nullptr};
+    hipStream_t spacer[8] = {};  // HK_GB_SPACERS / HK_DN_SPACERS experiments (streams without work)
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     // light targets
     uint2* albedo = nullptr;
@@ -612,6 +613,14 @@ int hk_create(int device, hk_ctx** out)
             hk_destroy(c);
             return HK_ERR_HIP;
         }
+    // experiment knobs: extra work-free streams created before the G-buffer / tail streams move them
+    // to other hardware queues (the round-robin mapping above)
+    auto spacers = [&](const char* var, int first) {
+        const char* e = getenv(var);
+        const int n = e ? std::min(4, std::max(0, atoi(e))) : 0;
+        for (int k = 0; k < n; ++k) (void)hipStreamCreateWithFlags(&c->spacer[first + k], hipStreamNonBlocking);
+    };
+    spacers("HK_GB_SPACERS", 0);
     if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         (HK_STREAM_LAYOUT == 1 ? (c->gb_stream = c->side[0], hipSuccess)
                                : hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -619,6 +628,7 @@ int hk_create(int device, hk_ctx** out)
         hipEventCreateWithFlags(&c->ev_gb_call[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess ||
+        (spacers("HK_DN_SPACERS", 4), false) ||
         (HK_STREAM_LAYOUT == 2 ? (c->dn_stream = c->side[0], hipSuccess)
                                : hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking)) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rf, hipEventDisableTiming) != hipSuccess ||
@@ -672,6 +682,8 @@ void hk_destroy(hk_ctx* c)
     if (c->gb_stream && c->gb_stream != c->side[0]) (void)hipStreamDestroy(c->gb_stream);
     if (c->dn_stream && c->dn_stream != c->side[0]) (void)hipStreamDestroy(c->dn_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (hipStream_t& sp : c->spacer)
+        if (sp) (void)hipStreamDestroy(sp);
     delete c;
 }
 
