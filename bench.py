@@ -79,7 +79,8 @@ BYTES_PER_PIXEL = {
 BG_ELIDED_BYTES = {"gbuffer": (None, 1, 1),  # a miss: its mask byte (the slot already holds the zero texels)
                    "direct_lit_emissive": ("emissive_spatial_reuse", 17, 145),
                    "indirect_lit_ambient": ("indirect_spatial_reuse", 17, 145),
-                   "indirect_multiple_bounces": ("indirect_spatial_reuse", 17, 145)}
+                   "indirect_multiple_bounces": ("indirect_spatial_reuse", 17, 145),
+                   "indirect_wavefront": ("indirect_spatial_reuse", 17, 145)}
 
 
 def kernel_bytes(name: str, covered_px: float, background_px: float, settings=None) -> float:

@@ -763,7 +763,7 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
     Reservoir r = zero_reservoir();
     const bool background = F.indirect_bounces == 0u || depth < HK_F32_EPSILON;
     uint32_t bg = BG_STORE;
-    if constexpr (STAGE == IND_ALL) bg = bg_elide(C, idx, background);
+    if constexpr (STAGE == IND_ALL || STAGE == IND_GEN) bg = bg_elide(C, idx, background);
     if (background) {
         if constexpr (STAGE == IND_ALL || STAGE == IND_GEN) {
             if (bg != BG_SKIP_ALL) {

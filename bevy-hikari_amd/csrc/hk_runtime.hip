@@ -1350,7 +1350,8 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     bool multi = settings->indirect_bounces >= 2u;
     // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
     const bool wf = c->wavefront && !multi && c->count[6] + 1u <= WF_MAX_BINS;
-    HK_TRY(bg_mask(c, 1, A, !wf && identity, !settings->indirect_spatial_reuse, s2, C2));
+    // (the wavefront pass elides in its generation stage, which classifies every pixel)
+    HK_TRY(bg_mask(c, 1, A, identity, !settings->indirect_spatial_reuse, s2, C2));
     if (wf) {
         HK_TRY(ensure_wavefront(c));
         WfArgs W{c->wf_queue1, c->wf_keys, c->wf_queue2, c->wf_hit, c->wf_hit_t, c->wf_ctl, c->count[6] + 1u,

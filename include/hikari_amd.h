@@ -281,7 +281,10 @@ int hk_get_output(hk_ctx* ctx, int output_id, void* dst, size_t bytes, int to_ho
 /* Device address of an output plane for zero-copy readers.  The planes of the G-buffer, render /
  * variance targets and albedo alternate between two slots from frame to frame, so the address is
  * valid for the current frame only; work on `stream` sees the plane's final contents after
- * hk_sync(ctx, stream) (the frame's G-buffer and tail may still run on the context's own streams). */
+ * hk_sync(ctx, stream) (the frame's G-buffer and tail may still run on the context's own streams).
+ * The planes are read-only for the caller: the light passes skip background stores whose targets
+ * already hold their constant words (background store elision), which a foreign write would break;
+ * planes and reservoirs are written through hk_set_gbuffer_plane / hk_load_reservoirs only. */
 const void* hk_output_device_ptr(hk_ctx* ctx, int output_id);
 /* Make `stream` wait (device-side) for all work the context queued on its own streams. */
 int hk_sync(hk_ctx* ctx, void* stream);
