@@ -451,6 +451,9 @@ def main():
             "primary_equivalent_mrays": round(W * H * spp * args.steps / elapsed / 1e6, 2),
             "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": spp,
                        "indirect": "wavefront material-sorted" if wavefront else "megakernel",
+                       # background pixels' constant stores skipped where their targets already hold
+                       # them (every buffer keeps the reference's bits; HK_NO_BG_ELIDE=1: off)
+                       "background_store_elision": os.environ.get("HK_NO_BG_ELIDE") != "1",
                        "rays_per_frame": int(rays // (args.steps * spp)),
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
