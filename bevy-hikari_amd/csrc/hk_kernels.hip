@@ -729,6 +729,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // compacted queue), IND_TRACE (the cosine bounce's closest hit, stored as an SoA hit record, keyed
 // by the hit's material), IND_SHADE (in material order: the rest of the pass from the stored hit).
 // The stages run the same statements in the same order for a pixel, so results are identical.
+#ifndef HK_IND_BG_EARLY  // experiment, measured slower (DESIGN §4 "Measured and not kept")
+#define HK_IND_BG_EARLY 0
+#endif
 enum IndStage : int { IND_ALL = 0, IND_GEN = 1, IND_TRACE = 2, IND_SHADE = 3 };
 HKD void wf_store_hit(const WfArgs& W, int32_t idx, const Hit& h)
 {
@@ -930,12 +933,26 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
 template <bool MULTI, bool LDS>
 __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, ChannelArgs C)
 {
-    Scene sc;
-    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
-    else sc = A.sc;
     int32_t x, y;
+    const bool active = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    Scene sc = A.sc;
+    if constexpr (LDS) {
+#if HK_IND_BG_EARLY
+        // a workgroup whose pixels are all background (sky; or no bounces) never walks: it skips
+        // the scene staging (indirect_body's background branch reads only the position texel)
+        bool live = false;
+        if (active && A.F.indirect_bounces != 0u) {
+            int32_t dx, dy;
+            jittered_coords(A.F, coords_to_uv(x, y, A.F.s), dx, dy);
+            live = load_position(A.F, A.G, dx, dy).w >= HK_F32_EPSILON;
+        }
+        if (__syncthreads_or(live)) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+#else
+        sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+#endif
+    }
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+    if (active) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
