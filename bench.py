@@ -60,9 +60,10 @@ BYTES_PER_PIXEL = {
     "indirect_lit_ambient": (184, 220),
     "indirect_multiple_bounces": (184, 220),
     "indirect_wavefront": (184, 220),    # the same compulsory streams (queues / hit records are extra traffic)
-    # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8 | position 16 + 64 + 64 + 8
-    "indirect_spatial_reuse": (244, 152),
-    "emissive_spatial_reuse": (244, 152),
+    # G 40 + temporal 64 + previous spatial 64 + spatial 64 + var 4 + render 8 | position 16 + spatial 64 +
+    # render 8 (the background record is repacked from registers: the temporal pass just stored it)
+    "indirect_spatial_reuse": (244, 88),
+    "emissive_spatial_reuse": (244, 88),
     "demodulation": (148, 148),      # reads G-buffer normal 4 + position 16 (RGBA32F texel, .w used) + ids 8 +
                                      # depth gradient 8 + albedo 8 + 3 x (render 8 + variance 4); writes geom 32
                                      # (the levels' per-pixel geometry) + 3 x (internal 8 + ivar 4)

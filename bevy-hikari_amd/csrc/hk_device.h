@@ -481,9 +481,8 @@ HKD Reservoir load_res(const ResBuf& b, int32_t i)
     const uint32_t u = (uint32_t)i;
     return unpack_reservoir(p[res_chunk(b, 0, u)], p[res_chunk(b, 1, u)], p[res_chunk(b, 2, u)], p[res_chunk(b, 3, u)]);
 }
-HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
+HKD void pack_res(const Reservoir& r, uint4& c0, uint4& c1, uint4& c2, uint4& c3)
 {
-    uint4 c0, c1, c2, c3;
     c3.z = pack2x16float(r.count, r.w);
     c3.w = pack2x16float(r.w_sum, r.w2_sum);
     c0.x = pack2x16float(r.s.radiance.x, r.s.radiance.y);
@@ -496,6 +495,11 @@ HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
                     __float_as_uint(r.s.sample_position.z), __float_as_uint((float)r.s.visible_instance));
     c3.x = hk_pack4x8snorm(r.s.visible_normal.x, r.s.visible_normal.y, r.s.visible_normal.z, r.lifetime / 127.0f - 1.0f);
     c3.y = hk_pack4x8snorm(r.s.sample_normal.x, r.s.sample_normal.y, r.s.sample_normal.z, r.s.sample_position.w);
+}
+HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
+{
+    uint4 c0, c1, c2, c3;
+    pack_res(r, c0, c1, c2, c3);
     uint4* p = b.base;
     const uint32_t u = (uint32_t)i;
     p[res_chunk(b, 0, u)] = c0;

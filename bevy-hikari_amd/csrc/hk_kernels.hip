@@ -729,6 +729,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // compacted queue), IND_TRACE (the cosine bounce's closest hit, stored as an SoA hit record, keyed
 // by the hit's material), IND_SHADE (in material order: the rest of the pass from the stored hit).
 // The stages run the same statements in the same order for a pixel, so results are identical.
+#ifndef HK_SPATIAL_BG_CONST
+#define HK_SPATIAL_BG_CONST 1
+#endif
 #ifndef HK_IND_BG_EARLY  // experiment, measured slower (DESIGN §4 "Measured and not kept")
 #define HK_IND_BG_EARLY 0
 #endif
@@ -1164,7 +1167,19 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
     float depth = pd.w;
     if (depth < HK_F32_EPSILON) {
+#if HK_SPATIAL_BG_CONST
+        // the temporal pass of this frame left its background record in C.cur at this pixel (it
+        // classifies the pixel from the same G-buffer texel, over a window that contains this
+        // pass's): the emissive pass's set_reservoir'd zero or the indirect pass's zero reservoir
+        // (light.wgsl:1063-1071, 1283-1290), so the record is repacked from registers, not re-read
+        {
+            uint4 c0, c1, c2, c3;
+            pack_res(EMISSIVE_LIT ? background_reservoir() : zero_reservoir(), c0, c1, c2, c3);
+            store_res(C.spatial, idx, unpack_reservoir(c0, c1, c2, c3));
+        }
+#else
         store_res(C.spatial, idx, load_res(C.cur, idx));
+#endif
         store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
         return;
     }
