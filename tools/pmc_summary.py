@@ -1,6 +1,11 @@
 """Summarise rocprofv3 --pmc passes written by tools/pmc.sh.
 
 usage: python tools/pmc_summary.py <pmc root dir> <config name> [--json profiles/pmc_traffic.json]
+                                   [--skip N] [--deep-json out.json "note"]
+
+--skip N drops each kernel's first N dispatches of every profiled run (the warm-up frames: before the
+background-store-elision masks settle, frames 0-1 store every background pixel), so the averages are
+steady-state.  --deep-json writes every counter per wave (SQ cycle counters in quad-cycles) per kernel.
 
 Prints per-kernel averages (per dispatch) of every collected counter plus derived figures, and
 with --json merges {config: {kernel: {...}}} into the traffic file bench.py reads.
@@ -39,7 +44,7 @@ def short(name: str) -> str:
     return name[:40]
 
 
-def load(root: Path):
+def load(root: Path, skip: int = 0):
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per dispatch]
     dur = defaultdict(list)
     for f in sorted(root.glob("**/*counter_collection.csv")):
@@ -53,13 +58,21 @@ def load(root: Path):
                 d = int(row["Dispatch_Id"])
                 per[d][row["Counter_Name"]] += float(row["Counter_Value"])
                 names[d] = k
-        for d, cs in per.items():
-            for c, v in cs.items():
+        seen = defaultdict(int)
+        for d in sorted(per):
+            seen[names[d]] += 1
+            if seen[names[d]] <= skip:
+                continue
+            for c, v in per[d].items():
                 vals[names[d]][c].append(v)
     for f in sorted(root.glob("**/*kernel_trace.csv")):
+        seen = defaultdict(int)
         with open(f) as fh:
-            for row in csv.DictReader(fh):
-                k = short(row["Kernel_Name"])
+            rows = sorted(csv.DictReader(fh), key=lambda r: int(r["Start_Timestamp"]))
+        for row in rows:
+            k = short(row["Kernel_Name"])
+            seen[k] += 1
+            if seen[k] > skip:
                 dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
     return vals, dur
 
@@ -87,10 +100,30 @@ def summarise(vals, dur):
     return out
 
 
+def deep(vals, dur):
+    out = {}
+    for k, cs in vals.items():
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        w = avg.get("SQ_WAVES")
+        if not w:
+            continue
+        e = {"per_wave": {c: round(v / w, 1) if c != "SQ_WAVES" else 1.0 for c, v in sorted(avg.items())},
+             "waves_per_launch": round(w, 1)}
+        if dur.get(k):
+            e["avg_ms_profiled"] = round(sum(dur[k]) / len(dur[k]), 4)
+        out[k] = e
+    return out
+
+
 def main():
     root, config = Path(sys.argv[1]), sys.argv[2]
-    vals, dur = load(root)
+    skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
+    vals, dur = load(root, skip)
     s = summarise(vals, dur)
+    if "--deep-json" in sys.argv:
+        i = sys.argv.index("--deep-json")
+        Path(sys.argv[i + 1]).write_text(json.dumps({"note": sys.argv[i + 2], "config": config, "skip": skip,
+                                                     "kernels": deep(vals, dur)}, indent=1))
     for k, e in sorted(s.items()):
         extra = {x: y for x, y in e.items() if x != "counters"}
         print(f"{k:28s} {extra}")
@@ -99,7 +132,7 @@ def main():
         d = json.loads(p.read_text()) if p.exists() else {}
         d.setdefault("note", "rocprofv3 --pmc (kernel-trace only), FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md "
                              "HBM section); x2 exact for 16-B/lane reads, 4/8-B texel reads uncalibrated")
-        d.setdefault("configs", {})[config] = {"kernels": s}
+        d.setdefault("configs", {})[config] = {"kernels": s, "skipped_warmup_dispatches": skip}
         p.write_text(json.dumps(d, indent=1))
 
 
