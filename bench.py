@@ -109,6 +109,15 @@ CONFIGS = {
     "city-4k-dynamic": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, dynamic=True,
                             workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, rotating "
                                      "emissive sphere: GPU instance/TLAS/light-BVH rebuild every frame"),
+    # configs[1] / configs[3] under camera motion: the examples' orbit camera (OrbitCameraBundle,
+    # cornell.rs:56-60, city.rs:134-138) yawing 0.5 deg per frame (examples.orbit).  Reprojection is no
+    # longer the identity, so the fused direct/emissive launch and background store elision are off
+    "cornell-1080p-nee-orbit": dict(scene="cornell", width=1920, height=1080, spatial=False, denoise=False, orbit=True,
+                                    workload="examples/cornell.rs 1920x1080 1spp, traversal + NEE only, orbit "
+                                             "camera (0.5 deg/frame)"),
+    "city-4k-orbit": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, orbit=True,
+                          workload="examples/city.rs layout (City proxy houses) 3840x2160 1spp, orbit camera "
+                                   "(0.5 deg/frame)"),
     # configs[0]: the reference's CPU-runnable case (a parity case; bench line for completeness)
     "cornell-256-all": dict(scene="cornell", width=256, height=256, spatial=True, denoise=True,
                             workload="examples/cornell.rs 256x256 1spp, all passes (ReSTIR temporal/spatial "
@@ -133,7 +142,7 @@ def cpu_threads() -> int:
     return max(1, min(n, 16))  # the GPU box grants 16 host cores to one GPU
 
 
-def cpu_baseline(scene_desc, cam, lights, st, w, h, budget_s: float) -> dict:
+def cpu_baseline(scene_desc, camera_at, lights, st, w, h, budget_s: float) -> dict:
     """The oracle (C restatement, OpenMP) on the same workload, bounded to ~budget_s seconds."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from oracle import Oracle  # test-infrastructure checker, used here only as the CPU baseline
@@ -144,7 +153,8 @@ def cpu_baseline(scene_desc, cam, lights, st, w, h, budget_s: float) -> dict:
     frames = 0
     t0 = time.perf_counter()
     while frames < 64:
-        fi = frame_inputs(frames, cam, lights, w, h)
+        cam, prev = camera_at(frames)
+        fi = frame_inputs(frames, cam, lights, w, h, previous_camera=prev)
         o.reset_counters()
         o.render_gbuffer(fi)
         o.render_frame(s, fi)
@@ -279,6 +289,16 @@ def main():
     spp = cfg.get("spp", 1)
     shown = hikari_amd._abi.OUT_TONE_MAPPED if spp == 1 else hikari_amd._abi.OUT_ACCUMULATED
 
+    # camera of frame f and of frame f - 1 (None: static, PreviousViewUniform = the current view)
+    if cfg.get("orbit"):
+        target = examples.ORBIT_TARGETS[cfg["scene"]]
+
+        def camera_at(f):
+            return examples.orbit(cam, target, f), (examples.orbit(cam, target, f - 1) if f > 0 else None)
+    else:
+        def camera_at(f):
+            return cam, None
+
     dynamic = cfg.get("dynamic", False)
     if dynamic:
         models0, aabbs = scene.instance_models(), scene.instance_local_aabbs()
@@ -295,7 +315,8 @@ def main():
             r.update_instances(models, aabbs, sp)
         # one displayed frame = spp integrator sub-frames, each exactly one reference frame
         for k in range(spp):
-            fi = frame_inputs(f * spp + k, cam, lights, W, H)
+            c, prev = camera_at(f * spp + k)
+            fi = frame_inputs(f * spp + k, c, lights, W, H, previous_camera=prev)
             r.render_gbuffer(fi, sp)
             r.render_frame(s, fi, sp)
             if st.denoise:
@@ -421,17 +442,22 @@ def main():
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         mrays = rays / elapsed / 1e6
-        # roofline of the dominant kernel (largest total time per frame)
-        per_frame = {}
-        for name, avg in timing.items():
-            launches = {"denoise": 4}.get(name, 1)
-            per_frame[name] = avg * launches
+        # Roofline of the dominant kernel, one definition: the kernel with the largest GPU
+        # time per frame when it runs alone (isolated frames; the timed region's overlapped durations
+        # when no isolated frames exist: bands, accumulation, dynamic scenes).
+        #   bytes_per_launch = SURVEY §8(d)'s reference-format bytes per pixel x the launch's pixels
+        #   achieved = bytes_per_launch / duration_ms, frac = achieved / 8 TB/s
+        #   traffic  = PMC-measured HBM bytes per launch (steady-state dispatches, profiles/pmc_traffic.json),
+        #              hbm_frac = traffic / duration_ms / 8 TB/s: the bandwidth the launch really draws
+        launches_per_frame = {"denoise": 4}
+        source = isolated if isolated else timing
+        per_frame = {k: v * launches_per_frame.get(k, 1) for k, v in source.items()}
         dom = max(per_frame, key=per_frame.get)
         pix = W * rows
         cov_px, bg_px = pix * coverage, pix * (1.0 - coverage)
-        alg = int(kernel_bytes(dom, cov_px, bg_px, st))
-        frame_bytes = int(sum(kernel_bytes(k, cov_px, bg_px, st) * {"denoise": 4}.get(k, 1) for k in timing) * spp)
-        achieved = alg / (timing[dom] * 1e-3) / 1e9
+        ref_bytes = int(BYTES_PER_PIXEL.get(dom, (0, 0))[0] * pix)
+        dur = source[dom]
+        achieved = ref_bytes / (dur * 1e-3) / 1e9
         # the committed PMC numbers are per launch of a whole 1-GPU frame; a band launch differs
         traffic = load_pmc_traffic(args.config, dom) if world == 1 else None
         result = {
@@ -446,7 +472,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (static camera; reference assets: cornell.glb, blue noise)",
+            "data": "synthetic ({} camera; reference assets: cornell.glb, blue noise)".format(
+                "orbiting" if cfg.get("orbit") else "static"),
             "latency_ms": None if latency is None else round(latency, 4),
             "primary_mrays": round(primary / elapsed / 1e6, 2),
             "primary_equivalent_mrays": round(W * H * spp * args.steps / elapsed / 1e6, 2),
@@ -461,40 +488,32 @@ def main():
                                        f"row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg, "coverage": round(coverage, 4),
-                         "avg_ms": round(timing[dom], 4),
-                         # all kernels of a frame together (they overlap: the indirect chain runs on a
-                         # side stream next to direct/emissive, so per-kernel durations include sharing)
-                         "frame_algorithmic_bytes": frame_bytes,
-                         "frame_achieved": round(frame_bytes / (ms * 1e-3) / 1e9, 1),
-                         "frame_frac": round(frame_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                         "hbm_frac": None if traffic is None else
+                         round(traffic / (dur * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "bytes_per_launch": ref_bytes, "bytes_per_pixel": BYTES_PER_PIXEL.get(dom, (0, 0))[0],
+                         "pixels_per_launch": pix, "duration_ms": round(dur, 4),
+                         "duration": "isolated" if isolated else "in frame (overlapped)"},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
             # each kernel alone on the GPU (the untimed isolated frames after the timed region)
             "isolated_kernel_ms": None if not isolated else {k: round(v, 4) for k, v in isolated.items()},
+            # context for the roofline (not fractions of it): the bytes the build's launch must move
+            # (background store elision skips constant stores), the share of covered pixels, and all
+            # of a frame's compulsory bytes over the frame time
+            "diagnostics": {"coverage": round(coverage, 4),
+                            "moved_bytes_per_launch": int(kernel_bytes(dom, cov_px, bg_px, st)),
+                            "frame_compulsory_bytes": int(sum(kernel_bytes(k, cov_px, bg_px, st) *
+                                                              launches_per_frame.get(k, 1) for k in timing) * spp)},
         }
-        if isolated and dom in isolated:
-            # the same kernel with the GPU to itself (8 untimed frames after the timed region)
-            iso = isolated[dom]
-            result["roofline"]["isolated_avg_ms"] = round(iso, 4)
-            result["roofline"]["isolated_achieved"] = round(alg / (iso * 1e-3) / 1e9, 1)
-            result["roofline"]["isolated_frac"] = round(alg / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-            # the bytes the reference moves for the same launch (no background store elision: every
-            # background pixel stores its zero reservoirs / texels again), over the same time
-            ref = kernel_bytes(dom, cov_px, bg_px)
-            if ref != alg:
-                result["roofline"]["reference_format_bytes_per_launch"] = int(ref)
-                result["roofline"]["isolated_reference_format_frac"] = round(ref / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         tb = load_traversal_bytes(args.config) if world == 1 and spp == 1 else None
         if tb is not None:
-            # §8d's second component: node / triangle / instance / hit_info bytes of the light passes
-            # (L1/L2/MALL traffic: the scene is cache resident), over the frame time
-            result["roofline"]["frame_traversal_bytes"] = tb
-            result["roofline"]["frame_traversal_achieved"] = round(tb / (ms * 1e-3) / 1e9, 1)
+            # SURVEY §8d's second component: node / triangle / instance / hit_info bytes of the light
+            # passes, priced in reference record sizes (L1/L2/MALL traffic: the scene is cache resident)
+            result["diagnostics"]["frame_traversal_bytes"] = tb
         lanes = load_lane_efficiency(args.config, wavefront)
         if lanes is not None:
-            result["roofline"]["lane_efficiency"] = lanes
+            result["diagnostics"]["lane_efficiency"] = lanes
         if world == 1 and args.cpu_budget > 0:
-            result["cpu_baseline"] = cpu_baseline(desc, cam, lights, st, W, H, args.cpu_budget)
+            result["cpu_baseline"] = cpu_baseline(desc, camera_at, lights, st, W, H, args.cpu_budget)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result))

@@ -56,16 +56,12 @@ HKD f3 mix(f3 a, f3 b, float t)
 // test_fast_reciprocal_is_exact): v_rcp_f32 (within 1 ulp) plus FMA residual corrections where
 // neither d nor 1/d is near the denormal range; the IEEE divide sequence elsewhere (0, inf, NaN,
 // |d| outside [2^-125, 2^125]).  Half the instructions of the divide.
-#ifndef HK_RCP_STEPS
-#define HK_RCP_STEPS 1
-#endif
 HKD float rcp_exact(float d)
 {
     const float a = fabsf(d);
     if (a >= 0x1p-125f && a <= 0x1p125f) {
         float r = __builtin_amdgcn_rcpf(d);
-#pragma unroll
-        for (int k = 0; k < HK_RCP_STEPS; ++k) r = fmaf(fmaf(-d, r, 1.0f), r, r);
+        r = fmaf(fmaf(-d, r, 1.0f), r, r);
         return r;
     }
     return 1.0f / d;
@@ -203,18 +199,14 @@ struct GBuffer {
     float4* velocity_uv;
 };
 
-// Reservoir buffer of N 64-byte PackedReservoir records, as 16-byte chunks.  HK_RES_AOS = 0: SoA,
-// 4 planes of N chunks (chunk k of record i at k * N + i: a wave's 64 consecutive records are one
-// 1-KiB coalesced load per chunk); 1: the reference's AoS order (chunk k of record i at 4 i + k: a
-// gathered record is one 64-byte segment instead of four).
-#ifndef HK_RES_AOS
-#define HK_RES_AOS 0
-#endif
+// Reservoir buffer of N 64-byte PackedReservoir records, as 16-byte chunks in SoA order: 4 planes of
+// N chunks (chunk k of record i at k * N + i: a wave's 64 consecutive records are one 1-KiB coalesced
+// load per chunk; the reference's AoS order measured slower).
 struct ResBuf {
     uint4* base;
     uint32_t n;  // records
 };
-__host__ __device__ __forceinline__ uint32_t res_chunk(const ResBuf& b, uint32_t k, uint32_t i) { return HK_RES_AOS ? 4u * i + k : k * b.n + i; }
+__host__ __device__ __forceinline__ uint32_t res_chunk(const ResBuf& b, uint32_t k, uint32_t i) { return k * b.n + i; }
 
 struct Counters {
     unsigned long long* top;
@@ -285,13 +277,6 @@ HKD float f16_val(uint32_t h)
     asm("v_cvt_f32_f16 %0, %1" : "=v"(r) : "v"(h));
     return r;
 }
-#ifdef HK_SOFT_F16
-#define f16_bits hk_f32_to_f16
-#define f16_val(h) hk_f16_to_f32((h) & 0xFFFFu)
-#endif
-#ifdef HK_SOFT_F16
-HKD uint32_t pack2x16float(float a, float b) { return f16_bits(a) | (f16_bits(b) << 16); }
-#else
 // asm as well: a plain fptrunc(fmul(a, b)) is selected as v_fma_mixlo_f16, which rounds the
 // exact product once to f16 instead of to f32 then f16 (the reference's two roundings).
 HKD uint32_t pack2x16float(float a, float b)
@@ -300,13 +285,9 @@ HKD uint32_t pack2x16float(float a, float b)
     asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-#endif
 HKD float unpack_lo16float(uint32_t v) { return f16_val(v); }
 HKD float unpack_hi16float(uint32_t v)
 {
-#ifdef HK_SOFT_F16
-    return f16_val(v >> 16);
-#endif
     float r;
     asm("v_cvt_f32_f16_sdwa %0, %1 src0_sel:WORD_1" : "=v"(r) : "v"(v));
     return r;
@@ -654,21 +635,13 @@ HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& 
     c = mk3(z.x, z.y, z.z);
 }
 
-#ifndef HK_TRAVERSE_PAIRSTEP
-#define HK_TRAVERSE_PAIRSTEP 1
-#endif
-#ifndef HK_WALK_STEPS
-#define HK_WALK_STEPS 2
-#endif
-#ifndef HK_WALK_EAGER
-#define HK_WALK_EAGER 0
-#endif
 
 // One iteration of the skip-pointer walk covering up to STEPS consecutive visits: node p and,
 // while the visited node is an inner node whose box passes, its subtree start (the next node of
 // the flattened array, bvh flatten).  All STEPS nodes are loaded and tested up front with the
 // same hit distance (no leaf work happens between such visits).  Returns the node the walk visits
 // next; `leaf_pass`/`leaf_entry` report the leaf reached in this iteration, if its box passed.
+constexpr int WALK_STEPS = 2;  // visits per walk iteration (3 and 4 measured slower)
 template <int STEPS>
 HKD uint32_t walk_step(const hk_node* nodes, uint32_t index, uint32_t count, const Ray& tr, float distance,
                        bool& leaf_pass, uint32_t& leaf_entry)
@@ -681,12 +654,6 @@ HKD uint32_t walk_step(const hk_node* nodes, uint32_t index, uint32_t count, con
         const uint32_t i = index + (uint32_t)k < count ? index + (uint32_t)k : index;  // in range; used only when visited
         load_node(nodes, i, mn[k], entry[k], mx[k], exit[k]);
     }
-#if HK_WALK_EAGER
-    // all STEPS node loads issued together (the compiler otherwise sinks node p + 1's load into
-    // the branch that uses it, after node p's test: two dependent load latencies per iteration)
-#pragma unroll
-    for (int k = 0; k < STEPS; ++k) __asm__ volatile("" ::"v"(mn[k].x), "v"(mx[k].x));
-#endif
 #pragma unroll
     for (int k = 0; k < STEPS; ++k) pass[k] = intersects_aabb(tr, mn[k], mx[k]) < distance;
     leaf_pass = false;
@@ -718,13 +685,12 @@ HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t nod
 {
     bool intersected = false;
     uint32_t index = 0u;
-#if HK_TRAVERSE_PAIRSTEP
-    // up to HK_WALK_STEPS visits per iteration (walk_step), as in traverse_top below
+    // up to WALK_STEPS visits per iteration (walk_step), as in traverse_top below
     const hk_node* nodes = sc.asset_nodes + node_offset;
     while (index < node_count) {
         bool leaf_pass;
         uint32_t leaf_entry;
-        const uint32_t next = walk_step<HK_WALK_STEPS>(nodes, index, node_count, ray, hit.distance, leaf_pass, leaf_entry);
+        const uint32_t next = walk_step<WALK_STEPS>(nodes, index, node_count, ray, hit.distance, leaf_pass, leaf_entry);
         if (leaf_pass) {
             uint32_t primitive_index = prim_offset + leaf_entry - HK_BVH_LEAF_FLAG;
             f3 a, b, c;
@@ -742,7 +708,6 @@ HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t nod
         index = next;
     }
     return intersected;
-#endif
     while (index < node_count) {
         f3 mn, mx;
         uint32_t entry, exit;
@@ -847,13 +812,12 @@ struct LaneStats {
 #define HK_LANE_STATS_TICK
 #endif
 
-#if HK_TRAVERSE_PAIRSTEP
 // Several visits per iteration where the order allows it (walk_step): an inner child-box node p
 // that passes is always followed by node p + 1 (its subtree start, bvh flatten), tested with the
 // same hit distance, so one iteration tests p and — while the visited nodes are passing inner
 // nodes — p + 1, p + 2, ... too, from consecutive node loads.  At most one of them is a leaf,
 // whose work (triangle test / instance entry) then follows.  Same visits, tests and results as
-// one node per iteration (HK_WALK_STEPS 2: cornell 1080p 0.619 -> 0.604 ms/frame).
+// one node per iteration (WALK_STEPS 2: cornell 1080p 0.619 -> 0.604 ms/frame).
 HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float early_distance, uint32_t exclude)
 {
     Hit hit;
@@ -881,7 +845,7 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
         // iteration reaches (if any) and the node after it
         bool leaf_pass;
         uint32_t leaf_entry;
-        const uint32_t next = walk_step<HK_WALK_STEPS>(nodes, index, count, tr, hit.distance, leaf_pass, leaf_entry);
+        const uint32_t next = walk_step<WALK_STEPS>(nodes, index, count, tr, hit.distance, leaf_pass, leaf_entry);
         if (in_bottom) {
             bool stop = false;
             if (leaf_pass) {
@@ -926,89 +890,6 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
     }
     return hit;
 }
-#else
-HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float early_distance, uint32_t exclude)
-{
-    Hit hit;
-    hit.uv = mk2(0.0f, 0.0f);
-    hit.distance = max_distance;
-    hit.instance_index = HK_U32_MAX;
-    hit.primitive_index = HK_U32_MAX;
-    uint32_t top = 0u;                  // next TLAS node
-    uint32_t bot = 0u, bot_count = 0u;  // BLAS walk state (in_bottom: inside an instance)
-    uint32_t bot_base = 0u, prim_offset = 0u, cur_instance = 0u;
-    bool in_bottom = false, intersected = false;
-    Ray local = ray;
-    HK_LANE_STATS_DECL;
-    for (;;) {
-        if (!in_bottom && top >= sc.n_instance_nodes) break;
-        HK_LANE_STATS_TICK;
-        const hk_node* nodes = in_bottom ? sc.asset_nodes + bot_base : sc.instance_nodes;
-        const uint32_t index = in_bottom ? bot : top;
-        f3 mn, mx;
-        uint32_t entry, exit;
-        load_node(nodes, index, mn, entry, mx, exit);
-        const bool leaf = entry >= HK_BVH_LEAF_FLAG;
-        // one slab test per iteration for every lane, with the lane's world or object-space ray;
-        // BLAS leaves carry their triangle's box (k_fill_blas_leaves, light.wgsl:411-413), TLAS
-        // leaves their instance's min/max (k_fill_tlas_leaves, light.wgsl:456-457)
-        Ray tr;
-        tr.origin = in_bottom ? local.origin : ray.origin;
-        tr.inv_direction = in_bottom ? local.inv_direction : ray.inv_direction;
-        const bool pass = intersects_aabb(tr, mn, mx) < hit.distance;
-        if (in_bottom) {
-            bool stop = false;
-            if (leaf) {
-                if (pass) {
-                    const uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
-                    f3 a, b, c;
-                    load_triangle(sc.primitives, primitive_index, a, b, c);
-                    f2 uv;
-                    const float d = intersects_triangle(local, a, b, c, uv);
-                    if (d < hit.distance) {
-                        hit.distance = d;
-                        hit.uv = uv;
-                        hit.primitive_index = primitive_index;
-                        intersected = true;
-                        stop = d < early_distance;  // traverse_bottom's early return
-                    }
-                }
-                bot = exit;
-            } else {
-                bot = pass ? entry : exit;
-            }
-            if (stop || bot >= bot_count) {  // back in traverse_top after traverse_bottom
-                in_bottom = false;
-                if (intersected) {
-                    hit.instance_index = cur_instance;
-                    if (hit.distance < early_distance) return hit;
-                }
-            }
-        } else {
-            if (leaf) {
-                const uint32_t instance_index = entry - HK_BVH_LEAF_FLAG;
-                if (instance_index != exclude && pass) {
-                    const hk_instance& in = sc.instances[instance_index];
-                    local.origin = world_to_local_point(in, ray.origin);
-                    local.direction = world_to_local_dir(in, ray.direction);
-                    local.inv_direction = inv(local.direction);
-                    bot = 0u;
-                    bot_count = in.mesh.node[1];
-                    bot_base = in.mesh.node[0];
-                    prim_offset = in.mesh.primitive;
-                    cur_instance = instance_index;
-                    intersected = false;
-                    in_bottom = bot_count > 0u;  // traverse_bottom over an empty range does nothing
-                }
-                top = exit;
-            } else {
-                top = pass ? entry : exit;
-            }
-        }
-    }
-    return hit;
-}
-#endif
 
 // ------------------------------------------------------------------ G-buffer visibility
 // Ordered closest-hit traversal, the build's own primary-visibility rule (the reference
@@ -1339,11 +1220,7 @@ HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 ra
         bool traced = false;
         if (dot(candidate.direction, normal) > 0.0f) {
             if (COUNT) n_emitter++;
-#ifdef HK_EXPERIMENT_NO_EMITTER_TRAVERSE  // timing experiment only (breaks parity)
-            traced = false;
-#else
             traced = traverse_bottom(sc, hit, r, ein.mesh.node[0], ein.mesh.node[1], ein.mesh.primitive, 0.0f);
-#endif
         }
         if (traced) {
             hit.instance_index = emissive.instance;

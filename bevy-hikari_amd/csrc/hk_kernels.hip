@@ -336,9 +336,6 @@ HKD DirectPixel load_direct_pixel(const FrameArgs& A, int32_t x, int32_t y)
 // select_light_candidate's emitter walk and traverse_top it sets the kernel's register peak
 // (143-147 VGPRs, 3 waves per SIMD).  Each thread writes its 28 words to its own LDS column before
 // the walks and reads them back after; the compiler barriers keep the registers dead in between.
-#ifndef HK_VALIDATE_PARK
-#define HK_VALIDATE_PARK 1
-#endif
 constexpr int PARK_WORDS = 39;  // the reservoir (28) + the sample's radiance / sample point (11): 39 KiB per
                                 // workgroup, so 4 workgroups (4 waves per SIMD) fit a CU's 160 KiB
 #define HK_PARK_FIELDS(X)                                                                                                  \
@@ -392,9 +389,6 @@ HKD float* park_area()
     return park;
 }
 
-#ifndef HK_FUSED_SHARE_SURFACE
-#define HK_FUSED_SHARE_SURFACE 1
-#endif
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, bool PARK = false>
 HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel P, uint32_t& n_top,
                      uint32_t& n_emitter, Surface* surface_out = nullptr, const Surface* surface_in = nullptr)
@@ -457,15 +451,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
         if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
         if (trace) {
             n_top++;
-#ifdef HK_EXPERIMENT_NO_SHADOW  // timing experiment only (breaks parity): shadow rays never hit
-            Hit hit;
-            hit.uv = mk2(0, 0);
-            hit.distance = HK_F32_MAX;
-            hit.instance_index = HK_U32_MAX;
-            hit.primitive_index = HK_U32_MAX;
-#else
             Hit hit = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
-#endif
             occlude_hit_info(ray, hit, info);
             s.radiance = EMISSIVE_LIT ? input_radiance(sc, F, ray, info, false, cand.emissive_instance, false)
                                       : input_radiance(sc, F, ray, info, true, DONT_SAMPLE_EMISSIVE, false);
@@ -669,15 +655,10 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
             store_res(C1.spatial, P.idx, z);
             store_res(C1.prev_spatial, P.idx, z);
         } else if (bg == BG_STORE) {
-#if HK_FUSED_SHARE_SURFACE
             // the pixel's surface (same material and uv in both passes) is fetched once
             Surface surface;
-            direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
-            direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
-#else
-            direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
-            direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
-#endif
+            direct_body<false, true, VD, !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
+            direct_body<true, false, VE, !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
         }
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
@@ -688,7 +669,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A,
 // The fused launch on frames that are not emissive-validation frames, held to 4 waves per SIMD
 // (128 VGPRs): without the emissive validation block the body needs 117-137 VGPRs (the direct
 // validation block on every third frame), a few of which then spill.
-// With the validation blocks parked in LDS (HK_VALIDATE_PARK, non-LDS-scene variants) the emissive
+// With the validation blocks parked in LDS (non-LDS-scene variants) the emissive
 // validation frames take this 4-wave kernel too (VE).
 template <bool LDS, bool VD, bool VE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_fused_w4(FrameArgs A, ChannelArgs C0,
@@ -707,15 +688,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             store_res(C1.spatial, P.idx, z);
             store_res(C1.prev_spatial, P.idx, z);
         } else if (bg == BG_STORE) {
-#if HK_FUSED_SHARE_SURFACE
             // the pixel's surface (same material and uv in both passes) is fetched once
             Surface surface;
-            direct_body<false, true, VD, HK_VALIDATE_PARK && !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
-            direct_body<true, false, VE, HK_VALIDATE_PARK && !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
-#else
-            direct_body<false, true, VD>(A, sc, C0, P, n_top, n_emitter);
-            direct_body<true, false, VE>(A, sc, C1, P, n_top, n_emitter);
-#endif
+            direct_body<false, true, VD, !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
+            direct_body<true, false, VE, !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
         }
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
@@ -729,12 +705,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // compacted queue), IND_TRACE (the cosine bounce's closest hit, stored as an SoA hit record, keyed
 // by the hit's material), IND_SHADE (in material order: the rest of the pass from the stored hit).
 // The stages run the same statements in the same order for a pixel, so results are identical.
-#ifndef HK_SPATIAL_BG_CONST
-#define HK_SPATIAL_BG_CONST 1
-#endif
-#ifndef HK_IND_BG_EARLY  // experiment, measured slower (DESIGN §4 "Measured and not kept")
-#define HK_IND_BG_EARLY 0
-#endif
 enum IndStage : int { IND_ALL = 0, IND_GEN = 1, IND_TRACE = 2, IND_SHADE = 3 };
 HKD void wf_store_hit(const WfArgs& W, int32_t idx, const Hit& h)
 {
@@ -940,19 +910,7 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
     const bool active = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
     Scene sc = A.sc;
     if constexpr (LDS) {
-#if HK_IND_BG_EARLY
-        // a workgroup whose pixels are all background (sky; or no bounces) never walks: it skips
-        // the scene staging (indirect_body's background branch reads only the position texel)
-        bool live = false;
-        if (active && A.F.indirect_bounces != 0u) {
-            int32_t dx, dy;
-            jittered_coords(A.F, coords_to_uv(x, y, A.F.s), dx, dy);
-            live = load_position(A.F, A.G, dx, dy).w >= HK_F32_EPSILON;
-        }
-        if (__syncthreads_or(live)) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
-#else
         sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
-#endif
     }
     uint32_t n_top = 0, n_emitter = 0;
     if (active) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
@@ -1167,7 +1125,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
     float depth = pd.w;
     if (depth < HK_F32_EPSILON) {
-#if HK_SPATIAL_BG_CONST
         // the temporal pass of this frame left its background record in C.cur at this pixel (it
         // classifies the pixel from the same G-buffer texel, over a window that contains this
         // pass's): the emissive pass's set_reservoir'd zero or the indirect pass's zero reservoir
@@ -1177,9 +1134,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             pack_res(EMISSIVE_LIT ? background_reservoir() : zero_reservoir(), c0, c1, c2, c3);
             store_res(C.spatial, idx, unpack_reservoir(c0, c1, c2, c3));
         }
-#else
-        store_res(C.spatial, idx, load_res(C.cur, idx));
-#endif
         store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
         return;
     }
@@ -1284,9 +1238,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 #if defined(HK_LANE_STATS) && HK_SP_STATS == 1  // lane statistics at the occlusion march (experiments)
         lane_stats_.tick();
 #endif
-#ifdef HK_EXPERIMENT_SP_NO_MARCH  // timing experiments only (break parity)
-        tap_count = 0u;
-#endif
         float inv_len = 1.0f / sqrtf(dot(offset, offset));
         f2 dir = mk2(offset.x * inv_len, offset.y * inv_len);
         const float sx = (float)F.s[0], sy = (float)F.s[1];
@@ -1323,9 +1274,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
                                   unpack_hi16float(c0.y));
         const f4 q_random = mk4(hk_unpack_unorm16(c0.z), hk_unpack_unorm16(c0.z >> 16), hk_unpack_unorm16(c0.w),
                                 hk_unpack_unorm16(c0.w >> 16));
-#ifdef HK_EXPERIMENT_SP_NO_SHADE
-        merge(q_radiance.x, q_w, q_count, q_random, nidx);
-#else
         float jacobian = 1.0f;
         if (hk_unpack_snorm8(c3.y, 3) > 0.5f) {
             // compute_jacobian(q.s, s) (light.wgsl:990-1004).  Its first vector, visible - q_sample,
@@ -1350,7 +1298,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             f3 o = shade(sc, sample_direction, q_radiance);
             merge(lum(o) / jacobian, q_w, q_count, q_random, nidx);
         }
-#endif
     }
     // the selected sample, re-read from its record (see SEL_OWN above)
     Reservoir r;
@@ -1684,7 +1631,7 @@ static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const Chan
                            uint32_t lds, hipStream_t st)
 {
     static const bool w4 = !getenv("HK_NO_FUSED_W4");
-    if (HK_VALIDATE_PARK && !LDS && w4 && ve) {
+    if (!LDS && w4 && ve) {
         if (vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
         else hipLaunchKernelGGL((k_direct_fused_w4<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
     } else if (vd && ve) hipLaunchKernelGGL((k_direct_fused<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);

@@ -187,11 +187,6 @@ int fail(hk_ctx* c, int code, const std::string& msg)
 
 hipStream_t pick(hk_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
 
-// experiment switch: 0 = G-buffer and tail streams of their own, 1 = the G-buffer on side[0],
-// 2 = the tail on side[0]
-#ifndef HK_STREAM_LAYOUT
-#define HK_STREAM_LAYOUT 0
-#endif
 
 #define HK_TRY(expr)            \
     do {                        \
@@ -530,9 +525,12 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
 // keep stale values that no windowed pass reads.  HK_BAND_FULL_WINDOWS=1: every pass on all rows.
 constexpr int32_t DENOISE_OUT_REACH = 16, SPATIAL_RANGE = 20, EMISSIVE_SPATIAL_RANGE = 10;
 constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
+// Only for a static frame: under camera or instance motion temporal reprojection reads the previous
+// frame's reservoirs at other rows, so every pass runs on the whole band (velocity_zero is set by
+// hk_render_gbuffer before its own window is taken).
 FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
 {
-    if (c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows) return A;
+    if (c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows || !c->velocity_zero) return A;
     static const bool full = getenv("HK_BAND_FULL_WINDOWS") && getenv("HK_BAND_FULL_WINDOWS")[0] == '1';
     if (full) return A;
     const int32_t lo = std::max(0, c->core_row0 - margin);
@@ -540,6 +538,13 @@ FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
     A.F.win_row0 = lo;
     A.F.win_rows = hi - lo;
     return A;
+}
+// HK_NO_BG_ELIDE=1 switches background store elision off (read per call: tests switch it per context;
+// the G-buffer's and the light passes' masks are both dropped while it is set)
+bool bg_elision_off()
+{
+    const char* e = getenv("HK_NO_BG_ELIDE");
+    return e && e[0] == '1';
 }
 int32_t light_out_reach(const hk_settings* st) { return st->denoise ? DENOISE_OUT_REACH : 0; }
 int32_t spatial_range(const hk_settings* st)
@@ -622,15 +627,13 @@ int hk_create(int device, hk_ctx** out)
     };
     spacers("HK_GB_SPACERS", 0);
     if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        (HK_STREAM_LAYOUT == 1 ? (c->gb_stream = c->side[0], hipSuccess)
-                               : hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking)) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess ||
         (spacers("HK_DN_SPACERS", 4), false) ||
-        (HK_STREAM_LAYOUT == 2 ? (c->dn_stream = c->side[0], hipSuccess)
-                               : hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking)) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rf, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rslot[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rslot[1], hipEventDisableTiming) != hipSuccess ||
@@ -1160,12 +1163,15 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     std::memcpy(V.previous_view_proj, pvp, sizeof(V.previous_view_proj));
     V.motion = (c->models_dirty || std::memcmp(pvp, in->view.view_proj, sizeof(V.previous_view_proj)) != 0) ? 1 : 0;
     V.previous_models = c->prev_models;
+    c->velocity_zero = V.motion == 0;
     // full_screen_albedo is fused into the G-buffer kernel (it has every input in registers);
     // hk_render_frame runs it on its own only for host-supplied G-buffers
     A = pass_window(c, A, GBUFFER_REACH);
     V.bg = nullptr;
     V.bg_need = 0;
-    if (!(getenv("HK_NO_BG_ELIDE") && getenv("HK_NO_BG_ELIDE")[0] == '1')) {
+    if (bg_elision_off()) {
+        c->gb_valid = false;  // the mask is rebuilt from zero when elision is switched back on
+    } else {
         if (!c->gb_valid || c->gb_key[0] != A.F.win_row0 || c->gb_key[1] != A.F.win_rows) {
             HK_HIP(c, hipMemsetAsync(c->gbmask, 0, (size_t)c->S[0] * c->S_rows, gs));
             c->gb_valid = true;
@@ -1181,7 +1187,6 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
                                    sizeof(hk_instance), 64, c->count[4], hipMemcpyDeviceToDevice, gs));
         c->models_dirty = false;
     }
-    c->velocity_zero = V.motion == 0;
     HK_HIP(c, hipEventRecord(c->ev_gb_done, gs));
     if (gs != st) c->gb_pending = true;
     c->gb_serial = false;
@@ -1248,10 +1253,9 @@ static ChannelArgs channel(hk_ctx* c, uint32_t number, int ch)
 // channel's targets this frame, so the mask is dropped and rebuilt from zero the next time).
 static int bg_mask(hk_ctx* c, int k, const FrameArgs& A, bool use, bool pair, hipStream_t st, ChannelArgs& C)
 {
-    static const bool off = getenv("HK_NO_BG_ELIDE") && getenv("HK_NO_BG_ELIDE")[0] == '1';
     C.bg = nullptr;
     C.bg_need = 0;
-    if (!use || off) {
+    if (!use || bg_elision_off()) {
         c->bg_valid[k] = false;
         return HK_OK;
     }

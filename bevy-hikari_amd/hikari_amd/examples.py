@@ -211,3 +211,20 @@ def city():
 
 
 SCENES = {"cornell": cornell, "cornell_textured": cornell_textured, "scene": scene_rs, "city": city}
+
+# OrbitCameraBundle targets of the examples (cornell.rs:56-60, scene.rs:123-142, city.rs:134-138); the
+# eyes are the scenes' camera translations
+ORBIT_TARGETS = {"cornell": (0.0, 1.0, 0.0), "cornell_textured": (0.0, 1.0, 0.0), "scene": (0.0, 0.0, 0.0),
+                 "city": (0.0, 0.0, 0.0)}
+ORBIT_YAW_PER_FRAME = math.radians(0.5)  # a steady mouse orbit: 30 deg/s at 60 frames/s
+
+
+def orbit(camera: Camera, target, frame: int, yaw_per_frame: float = ORBIT_YAW_PER_FRAME) -> Camera:
+    """The examples' orbit camera (OrbitCameraController, user-driven in the reference) as a deterministic
+    benchmark motion: the eye yawed about the vertical axis through `target` by frame * yaw_per_frame,
+    looking at the target."""
+    t = np.asarray(camera.transform.translation, np.float64) - np.asarray(target, np.float64)
+    a = yaw_per_frame * frame
+    c, s = math.cos(a), math.sin(a)
+    eye = np.array([c * t[0] + s * t[2], t[1], -s * t[0] + c * t[2]]) + np.asarray(target, np.float64)
+    return Camera(Transform.from_xyz(*eye).looking_at(tuple(target)))

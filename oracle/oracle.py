@@ -157,6 +157,15 @@ class Oracle:
         p = self._L.hko_reservoirs(self.ctx, buffer_id, C.byref(cnt))
         return np.frombuffer(C.string_at(p, cnt.value * 64), RESERVOIR_DTYPE).copy()
 
+    def load_reservoirs(self, buffer_id: int, records: np.ndarray):
+        """Overwrite reservoir buffer `buffer_id` (the first len(records) records), as hk_load_reservoirs."""
+        cnt = C.c_uint32()
+        p = self._L.hko_reservoirs(self.ctx, buffer_id, C.byref(cnt))
+        data = np.ascontiguousarray(records).view(np.uint8)
+        if data.nbytes > cnt.value * 64:
+            raise ValueError("more records than the buffer holds")
+        C.memmove(p, data.ctypes.data, data.nbytes)
+
     def counters(self) -> dict:
         v = (C.c_uint64 * 3)()
         self._L.hko_counters(self.ctx, v)

@@ -100,6 +100,37 @@ def test_moving_camera_bit_exact(size):
     assert r.counters() == o.counters()
 
 
+def test_moving_camera_1080p_bit_exact():
+    """The bench's moving-camera workload at full size (bench.py cornell-1080p-nee-orbit: cornell
+    1920x1080, traversal + NEE, the examples' orbit camera at 0.5 deg/frame, examples.orbit): 3 frames,
+    every plane bit-exact, the spatial-pair scatter targets within the stated tolerance.  With motion
+    the fused direct/emissive launch and background store elision are off: this covers the separate
+    launches at bench size."""
+    from hikari_amd import HikariSettings, Taa, Upscale, examples, frame_inputs
+    w, h = 1920, 1080
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, taa=Taa.None_, indirect_spatial_reuse=False, denoise=False)
+    scene, cam, lights, r, o = _pair("cornell", w, h, st)
+    s = st.to_c()
+    target = examples.ORBIT_TARGETS["cornell"]
+    errors, stats = [], []
+    moved = 0
+    for f in range(3):
+        fi = frame_inputs(f, examples.orbit(cam, target, f), lights, w, h,
+                          previous_camera=examples.orbit(cam, target, f - 1) if f else None)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.tone_sum(s)
+        _compare(r, o, f, errors, outputs=(0, 1, 2, 3, 4, 5, 6, 10, 11, 12, 13, 14, 15), stats=stats)
+        vel = r.output(15).view(np.float32).reshape(h, w, 4)[..., :2]
+        moved += int((vel != 0).any(axis=-1).sum())
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
+    assert moved > w * h // 4
+    assert r.counters() == o.counters()
+
+
 def test_moving_camera_spatial_reuse_within_tolerance():
     """Moving camera with indirect spatial reuse and the denoiser: spatial reuse reads the racy
     scatter target (load_previous_spatial_reservoir at previous_uv, light.wgsl:1581-1583), so its
@@ -339,6 +370,42 @@ def test_background_elision_bit_exact(monkeypatch, launch):
                 m = mismatch_report(g, c0, f"frame {f} reservoir {rid} background records")
                 if m:
                     errors.append(m)
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
+
+
+@pytest.mark.parametrize("jitter", [0, 1], ids=["static", "taa_jitter"])
+def test_background_elision_spatial_pairs_bit_exact(monkeypatch, jitter):
+    """Background store elision with both spatial reuse passes on (emissive_spatial_reuse and
+    indirect_spatial_reuse): the fused launch's background pixels then skip their own targets but
+    still store the spatial pair (the spatial passes rewrite it with a repacked record), and with TAA
+    jitter the silhouettes move every frame while the velocity stays zero, so elision stays on over a
+    changing coverage.  Static camera (no scatter race): every plane and all 10 reservoir buffers
+    bit-exact on every frame, including after garbage is uploaded over the spatial pairs."""
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    from hikari_amd.plugin import RESERVOIR_DTYPE
+    monkeypatch.setenv("HK_FUSE_MIN_PX", "0")
+    w, h = 64, 48
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, emissive_spatial_reuse=True, indirect_spatial_reuse=True,
+                        denoise=True)
+    scene, cam, lights, r, o = _pair("cornell", w, h, st, threads=0)
+    s = st.to_c()
+    errors = []
+    rng = np.random.default_rng(9)
+    for f in range(9):
+        if f == 7:  # garbage over both spatial pairs, on both sides: the elision masks must be dropped
+            for rid in RACY:
+                garbage = np.frombuffer(rng.bytes(w * h * RESERVOIR_DTYPE.itemsize), RESERVOIR_DTYPE)
+                r.load_reservoirs(rid, garbage)
+                o.load_reservoirs(rid, garbage)
+        fi = frame_inputs(f, cam, lights, w, h, jitter=jitter)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        _compare(r, o, f, errors, racy=())
         if errors:
             break
     assert not errors, "\n".join(errors[:20])

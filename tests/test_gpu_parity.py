@@ -81,22 +81,44 @@ def test_cornell_frames_bit_exact(size, lds_mode):
 @pytest.mark.parametrize("config,frames", [("cornell-1080p-nee", 4), ("scene-1080p-full", 2), ("city-4k", 2)])
 def test_full_size_bench_workloads_bit_exact(config, frames):
     """The bench workloads themselves (BASELINE configs 2-4 at 1920x1080 and 3840x2160): every output plane
-    of every frame, all reservoir buffers of the last frame and the ray counters bit-exact."""
+    of every frame, all reservoir buffers of the last frame and the ray counters bit-exact; for city 4K
+    the 8-band decomposition of configs[3] too (each band's core rows of the tone-mapped frame)."""
     import bench
-    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, frame_inputs
+    from hikari_amd.bands import band_of, halo_rows
     cfg = bench.CONFIGS[config]
     w, h = cfg["width"], cfg["height"]
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
     scene, cam, lights, r, o = _setup(w, h, st, cfg["scene"])
     s = st.to_c()
+    # city 4K: also BASELINE configs[3]'s own decomposition, 8 row bands of 270 rows + halo (one context
+    # per band, as the 8 ranks of bench.py --gpus 8 hold them), core rows against the whole-frame oracle
+    bands = []
+    if config == "city-4k":
+        for k in range(8):
+            b = band_of(k, 8, h)
+            rb = HikariRenderer(0)
+            rb.set_noise()
+            rb.upload_scene(scene)
+            rb.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
+            rb.resize(w, h, 1.0, b.y0, b.rows)
+            bands.append((b, rb))
     errors = []
     for f in range(frames):
         fi = frame_inputs(f, cam, lights, w, h)
-        for x in (r, o):
+        for x in [r, o] + [rb for _, rb in bands]:
             x.render_gbuffer(fi)
             x.render_frame(s, fi)
             x.denoise(s, fi)
             x.tone_sum(s)
+        whole = canon_plane(10, o.output(10))
+        for b, rb in bands:
+            row0, rows, core0, core_rows = rb.band_info()
+            assert row0 + core0 == b.y0 and core_rows == b.rows == h // 8
+            m = mismatch_report(canon_plane(10, rb.output(10)[core0: core0 + core_rows]), whole[b.y0: b.y0 + b.rows],
+                                f"frame {f} band {b.y0}+{b.rows} output 10")
+            if m:
+                errors.append(m)
         for oid in OUTPUTS:
             m = mismatch_report(canon_plane(oid, r.output(oid)), canon_plane(oid, o.output(oid)), f"frame {f} output {oid}")
             if m:
@@ -276,6 +298,57 @@ def test_gpu_row_bands_match_whole_frame(spatial, denoise, world, H):
         for k, v in r.counters().items():
             total[k] += v
     assert total == o.counters()
+
+
+def test_gpu_row_bands_moving_camera_within_tolerance():
+    """Band contexts under camera motion (the examples' orbit, examples.orbit at 2 deg/frame): every pass
+    then runs on the whole band (pass_window keeps row windows for static frames only), and temporal
+    reprojection reads previous reservoirs that the band computed itself.  The reference's own scatter
+    race (light.wgsl:1092-1095) and rows reprojected from beyond a band's halo make this inexact by
+    nature, so the tone-mapped core rows must match the whole-frame oracle on >= 95 % of
+    pixels with a mean relative difference <= 2 %, over 5 frames with spatial reuse and the denoiser."""
+    import math
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
+    from hikari_amd.bands import band_of, halo_rows
+    from oracle import Oracle
+    W, H, world = 64, 192, 3
+    scene, cam, lights = examples.cornell()
+    desc = scene.build()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=True)
+    s = st.to_c()
+    o = Oracle(desc, load_noise(), W, H, 1.0, threads=1)
+    ranks = []
+    for k in range(world):
+        b = band_of(k, world, H)
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.set_band_halo(halo_rows(True, True))
+        r.resize(W, H, 1.0, b.y0, b.rows)
+        ranks.append((b, r))
+    target = examples.ORBIT_TARGETS["cornell"]
+    yaw = math.radians(2.0)
+    errors = []
+    for f in range(5):
+        fi = frame_inputs(f, examples.orbit(cam, target, f, yaw), lights, W, H,
+                          previous_camera=examples.orbit(cam, target, f - 1, yaw) if f else None)
+        for x in [o] + [r for _, r in ranks]:
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        whole = canon_plane(10, o.output(10)).reshape(H, W, 4)
+        for b, r in ranks:
+            row0, rows, core0, core_rows = r.band_info()
+            a = canon_plane(10, r.output(10)[core0: core0 + core_rows]).reshape(core_rows, W, 4)
+            c = whole[b.y0: b.y0 + b.rows]
+            exact = float((a == c).all(axis=-1).mean())
+            fa = a.view(np.float16).astype(np.float32)[..., :3]
+            fc = c.view(np.float16).astype(np.float32)[..., :3]
+            rel = float(np.abs(fa - fc).sum() / max(np.abs(fc).sum(), 1e-6))
+            if exact < 0.95 or rel > 0.02:
+                errors.append(f"frame {f} band {b.y0}: {exact:.4f} of pixels exact, mean relative difference {rel:.4f}")
+    assert not errors, "\n".join(errors)
 
 
 @pytest.mark.parametrize("world", [2, 3])

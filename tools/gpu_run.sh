@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU call of round 2: a test selection, then bench lines.  usage (on the GPU box):
-#   bash tools/gpu_round2.sh <tag> "<pytest args>" [bench configs...]
+# One GPU call: a test selection, then bench lines.  usage (on the GPU box):
+#   bash tools/gpu_run.sh <tag> "<pytest args>" [bench configs...]
 # every GPU step has its own time limit; the script stops at the first failing step.
 set -e
 TAG=$1
@@ -20,6 +20,6 @@ for spec in "$@"; do
   ENVS=""
   [ -n "$envs" ] && ENVS=$(echo $envs | tr ',' ' ')
   env $ENVS timeout -k 10 300 python bench.py --config $cfg $BENCH_ARGS > $OUT/bench_$name.json 2> $OUT/bench_$name.err || { tail -20 $OUT/bench_$name.err; exit 1; }
-  echo "$name: $(python -c "import json;d=json.load(open('$OUT/bench_$name.json'));print(d['value'], d['ms_per_step'], d.get('latency_ms'), d['roofline']['kernel'], d['roofline']['frac'], d['kernel_ms'])")"
+  echo "$name: $(python -c "import json;d=json.load(open('$OUT/bench_$name.json'));print(d['value'], d['ms_per_step'], d.get('latency_ms'), d['roofline']['kernel'], d['roofline']['frac'], d['roofline']['duration_ms'], d['kernel_ms'])")"
 done
 echo done

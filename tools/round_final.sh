@@ -7,9 +7,9 @@ TAG=${1:-round_final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 bash tools/final_check.sh $TAG
-BENCH_ARGS='--steps 20 --warmup 4 --cpu-budget 0' bash tools/gpu_round2.sh $TAG '' \
+BENCH_ARGS='--steps 20 --warmup 4 --cpu-budget 0' bash tools/gpu_run.sh $TAG '' \
   scene:scene-1080p-full city:city-4k cornell256:cornell-256-all city-dynamic:city-4k-dynamic
-BENCH_ARGS='--steps 2 --warmup 1 --cpu-budget 0' bash tools/gpu_round2.sh $TAG '' \
+BENCH_ARGS='--steps 2 --warmup 1 --cpu-budget 0' bash tools/gpu_run.sh $TAG '' \
   city16-wavefront:city-4k-16spp city16-megakernel:city-4k-16spp:HK_BENCH_WAVEFRONT=0
 timeout -k 10 300 python tools/band_scaling.py cornell-1080p-nee 50 > gpurun_out/$TAG/bands_cornell.log 2>&1
 timeout -k 10 300 python tools/band_scaling.py scene-1080p-full 30 --bands > gpurun_out/$TAG/bands_scene.log 2>&1
