@@ -351,7 +351,7 @@ HKD f3 load_normal(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
     if (!in_frame(x, y, F.S)) return mk3(0, 0, 0);
     uint32_t n = G.normal[band_index(F, x, y, F.S[0], F.S_row0, F.S_rows)];
-    return mk3(hk_unpack_snorm8(n, 0), hk_unpack_snorm8(n, 1), hk_unpack_snorm8(n, 2));
+    return mk3(hk_unpack_snorm8_fast(n, 0), hk_unpack_snorm8_fast(n, 1), hk_unpack_snorm8_fast(n, 2));
 }
 HKD f2 load_instance_material(const Frame& F, const GBuffer& G, int32_t x, int32_t y)
 {
@@ -444,15 +444,15 @@ HKD Reservoir unpack_reservoir(uint4 c0, uint4 c1, uint4 c2, uint4 c3)
     r.w2_sum = unpack_hi16float(c3.w);
     r.s.radiance = mk4(unpack_lo16float(c0.x), unpack_hi16float(c0.x), unpack_lo16float(c0.y),
                        unpack_hi16float(c0.y));
-    r.s.random = mk4(hk_unpack_unorm16(c0.z), hk_unpack_unorm16(c0.z >> 16), hk_unpack_unorm16(c0.w),
-                     hk_unpack_unorm16(c0.w >> 16));
+    r.s.random = mk4(hk_unpack_unorm16_fast(c0.z), hk_unpack_unorm16_fast(c0.z >> 16), hk_unpack_unorm16_fast(c0.w),
+                     hk_unpack_unorm16_fast(c0.w >> 16));
     r.s.visible_position = mk4(__uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z), __uint_as_float(c1.w));
     uint32_t vn = c3.x;
-    r.s.visible_normal = normalize(mk3(hk_unpack_snorm8(vn, 0), hk_unpack_snorm8(vn, 1), hk_unpack_snorm8(vn, 2)));
-    r.lifetime = 127.0f * (1.0f + hk_unpack_snorm8(vn, 3));
+    r.s.visible_normal = normalize(mk3(hk_unpack_snorm8_fast(vn, 0), hk_unpack_snorm8_fast(vn, 1), hk_unpack_snorm8_fast(vn, 2)));
+    r.lifetime = 127.0f * (1.0f + hk_unpack_snorm8_fast(vn, 3));
     uint32_t sn = c3.y;
-    r.s.sample_position = mk4(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z), hk_unpack_snorm8(sn, 3));
-    r.s.sample_normal = normalize(mk3(hk_unpack_snorm8(sn, 0), hk_unpack_snorm8(sn, 1), hk_unpack_snorm8(sn, 2)));
+    r.s.sample_position = mk4(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z), hk_unpack_snorm8_fast(sn, 3));
+    r.s.sample_normal = normalize(mk3(hk_unpack_snorm8_fast(sn, 0), hk_unpack_snorm8_fast(sn, 1), hk_unpack_snorm8_fast(sn, 2)));
     r.s.visible_instance = f2u32(__uint_as_float(c2.w));
     return r;
 }
@@ -474,7 +474,7 @@ HKD void pack_res(const Reservoir& r, uint4& c0, uint4& c1, uint4& c2, uint4& c3
                     __float_as_uint(r.s.visible_position.z), __float_as_uint(r.s.visible_position.w));
     c2 = make_uint4(__float_as_uint(r.s.sample_position.x), __float_as_uint(r.s.sample_position.y),
                     __float_as_uint(r.s.sample_position.z), __float_as_uint((float)r.s.visible_instance));
-    c3.x = hk_pack4x8snorm(r.s.visible_normal.x, r.s.visible_normal.y, r.s.visible_normal.z, r.lifetime / 127.0f - 1.0f);
+    c3.x = hk_pack4x8snorm(r.s.visible_normal.x, r.s.visible_normal.y, r.s.visible_normal.z, div_by(r.lifetime, 127.0f, HK_INV_127) - 1.0f);  // div_by: exact for 127 (test_fast_division_by_frame_size_is_exact)
     c3.y = hk_pack4x8snorm(r.s.sample_normal.x, r.s.sample_normal.y, r.s.sample_normal.z, r.s.sample_position.w);
 }
 HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)

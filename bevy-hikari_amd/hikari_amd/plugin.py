@@ -24,6 +24,14 @@ RESERVOIR_DTYPE = np.dtype([("radiance", "<u4", 2), ("random", "<u4", 2), ("visi
 assert RESERVOIR_DTYPE.itemsize == 64
 
 
+def _stream(stream):
+    """A hipStream_t handle for the C ABI: None (the context's own stream) or an integer address
+    (e.g. torch.cuda.Stream.cuda_stream); anything else is refused here, before it reaches HIP."""
+    if stream is None or isinstance(stream, int):
+        return stream
+    raise TypeError(f"stream must be None or an integer hipStream_t handle, not {type(stream).__name__}")
+
+
 def _check(ctx, rc: int, what: str) -> None:
     if rc != 0:
         msg = _abi.lib().hk_last_error(ctx).decode() if ctx else ""
@@ -76,7 +84,7 @@ class HikariRenderer:
 
     def copy_output_rows(self, output_id: int, row0: int, rows: int, dst_ptr: int, to_host: bool = False,
                          stream=None) -> None:
-        _check(self.ctx, self._L.hk_copy_output_rows(self.ctx, output_id, row0, rows, dst_ptr, int(to_host), stream),
+        _check(self.ctx, self._L.hk_copy_output_rows(self.ctx, output_id, row0, rows, dst_ptr, int(to_host), _stream(stream)),
                "hk_copy_output_rows")
 
     def band_info(self):
@@ -86,17 +94,17 @@ class HikariRenderer:
 
     # ---- per frame
     def render_gbuffer(self, inputs: _abi.hk_frame_inputs, stream=None) -> None:
-        _check(self.ctx, self._L.hk_render_gbuffer(self.ctx, C.byref(inputs), stream), "hk_render_gbuffer")
+        _check(self.ctx, self._L.hk_render_gbuffer(self.ctx, C.byref(inputs), _stream(stream)), "hk_render_gbuffer")
 
     def render_frame(self, settings: _abi.hk_settings, inputs: _abi.hk_frame_inputs, stream=None) -> None:
-        _check(self.ctx, self._L.hk_render_frame(self.ctx, C.byref(settings), C.byref(inputs), stream),
+        _check(self.ctx, self._L.hk_render_frame(self.ctx, C.byref(settings), C.byref(inputs), _stream(stream)),
                "hk_render_frame")
 
     def denoise(self, settings: _abi.hk_settings, inputs: _abi.hk_frame_inputs, stream=None) -> None:
-        _check(self.ctx, self._L.hk_denoise(self.ctx, C.byref(settings), C.byref(inputs), stream), "hk_denoise")
+        _check(self.ctx, self._L.hk_denoise(self.ctx, C.byref(settings), C.byref(inputs), _stream(stream)), "hk_denoise")
 
     def tone_sum(self, settings: _abi.hk_settings, stream=None) -> None:
-        _check(self.ctx, self._L.hk_tone_sum(self.ctx, C.byref(settings), stream), "hk_tone_sum")
+        _check(self.ctx, self._L.hk_tone_sum(self.ctx, C.byref(settings), _stream(stream)), "hk_tone_sum")
 
     def update_instances(self, models: np.ndarray, local_aabbs: np.ndarray, stream=None) -> None:
         """New transforms of every instance (hk_update_instances): (n, 16) column-major models and
@@ -106,7 +114,7 @@ class HikariRenderer:
         a = np.ascontiguousarray(local_aabbs, np.float32).reshape(-1, 6)
         if len(m) != len(a):
             raise ValueError("models and local_aabbs differ in length")
-        _check(self.ctx, self._L.hk_update_instances(self.ctx, m.ctypes.data, a.ctypes.data, len(m), stream),
+        _check(self.ctx, self._L.hk_update_instances(self.ctx, m.ctypes.data, a.ctypes.data, len(m), _stream(stream)),
                "hk_update_instances")
 
     def scene_array(self, array: int, dtype, count: int) -> np.ndarray:
@@ -118,16 +126,16 @@ class HikariRenderer:
 
     def post_process(self, settings: _abi.hk_settings, inputs: _abi.hk_frame_inputs, stream=None) -> None:
         """SMAA TU4x + TAA Jasmine after tone mapping (hk_post_process)."""
-        _check(self.ctx, self._L.hk_post_process(self.ctx, C.byref(settings), C.byref(inputs), stream),
+        _check(self.ctx, self._L.hk_post_process(self.ctx, C.byref(settings), C.byref(inputs), _stream(stream)),
                "hk_post_process")
 
     def accumulate(self, reset: bool = False, stream=None) -> None:
         """Add the tone-mapped output to the sub-frame accumulator (hk_accumulate)."""
-        _check(self.ctx, self._L.hk_accumulate(self.ctx, int(reset), stream), "hk_accumulate")
+        _check(self.ctx, self._L.hk_accumulate(self.ctx, int(reset), _stream(stream)), "hk_accumulate")
 
     def resolve_accumulation(self, stream=None) -> None:
         """Accumulator / sub-frame count -> OUT_ACCUMULATED (RGBA16F)."""
-        _check(self.ctx, self._L.hk_resolve_accumulation(self.ctx, stream), "hk_resolve_accumulation")
+        _check(self.ctx, self._L.hk_resolve_accumulation(self.ctx, _stream(stream)), "hk_resolve_accumulation")
 
     # ---- readback
     def output_info(self, output_id: int):
@@ -154,13 +162,13 @@ class HikariRenderer:
 
     def sync(self, stream=None) -> None:
         """`stream` waits for the context's own streams (hk_sync)."""
-        _check(self.ctx, self._L.hk_sync(self.ctx, stream), "hk_sync")
+        _check(self.ctx, self._L.hk_sync(self.ctx, _stream(stream)), "hk_sync")
 
     def set_gbuffer_plane(self, plane: int, data: np.ndarray, stream=None) -> None:
         """A host G-buffer plane (hk_set_gbuffer_plane; 0..4 = position, normal, depth gradient,
         instance/material, velocity/uv), the route that keeps the reference's raster prepass."""
         d = np.ascontiguousarray(data)
-        _check(self.ctx, self._L.hk_set_gbuffer_plane(self.ctx, plane, d.ctypes.data, d.nbytes, 0, stream),
+        _check(self.ctx, self._L.hk_set_gbuffer_plane(self.ctx, plane, d.ctypes.data, d.nbytes, 0, _stream(stream)),
                "hk_set_gbuffer_plane")
 
     def reservoirs(self, buffer_id: int) -> np.ndarray:

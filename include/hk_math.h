@@ -236,6 +236,26 @@ HK_HD float hk_unpack_snorm8(uint32_t v, int c)
     return hk_maxf((float)i / 127.0f, -1.0f);
 }
 
+/* The same two decodes without the divide, for the device kernels (the oracle keeps the divisions
+ * above as its restatement): q0 = v * RN(1/d) and one residual correction give RN(v / d) for every
+ * input of these integer domains — all 65,536 unorm16 and all 256 snorm8 codes, checked exhaustively
+ * by hko_unpack_fast_mismatches (tests/test_oracle_kat.py) and, for the formula itself, in exact
+ * rational arithmetic.  3 instructions instead of the IEEE divide sequence. */
+#define HK_INV_65535 0x1.00010p-16f /* RN(1 / 65535) */
+#define HK_INV_127 0x1.020408p-7f   /* RN(1 / 127) */
+HK_HD float hk_unpack_unorm16_fast(uint32_t v)
+{
+    const float x = (float)(v & 0xFFFFu);
+    const float q = x * HK_INV_65535;
+    return fmaf(fmaf(-q, 65535.0f, x), HK_INV_65535, q);
+}
+HK_HD float hk_unpack_snorm8_fast(uint32_t v, int c)
+{
+    const float x = (float)(int32_t)(int8_t)((v >> (8 * c)) & 0xFFu);
+    const float q = x * HK_INV_127;
+    return hk_maxf(fmaf(fmaf(-q, 127.0f, x), HK_INV_127, q), -1.0f);
+}
+
 /* utils.wgsl:15-29 */
 HK_HD uint32_t hk_hash(uint32_t value)
 {

@@ -2386,6 +2386,17 @@ void hko_pack_reservoir_roundtrip(const float* f, hk_packed_reservoir* packed, f
     u[21] = q.s.sample_position.x; u[22] = q.s.sample_position.y; u[23] = q.s.sample_position.z; u[24] = q.s.sample_position.w;
     u[25] = q.s.sample_normal.x; u[26] = q.s.sample_normal.y; u[27] = q.s.sample_normal.z;
 }
+/* hk_unpack_unorm16_fast / hk_unpack_snorm8_fast (the device kernels' divide-free decodes) against
+ * the divisions over their whole input domains: the number of codes whose bits differ */
+uint32_t hko_unpack_fast_mismatches(void)
+{
+    uint32_t bad = 0;
+    for (uint32_t v = 0; v < 65536u; ++v)
+        if (hk_f2u(hk_unpack_unorm16_fast(v)) != hk_f2u(hk_unpack_unorm16(v))) ++bad;
+    for (uint32_t v = 0; v < 256u; ++v)
+        if (hk_f2u(hk_unpack_snorm8_fast(v << 8, 1)) != hk_f2u(hk_unpack_snorm8(v << 8, 1))) ++bad;
+    return bad;
+}
 float hko_pow(float x, float y) { return hk_pow(x, y); }
 float hko_pow_int(float x, int n) { return n == 2 ? hk_pow2(x) : (n == 5 ? hk_pow5(x) : hk_pow16(x)); }
 float hko_exp2(float x) { return hk_exp2(x); }

@@ -61,6 +61,7 @@ def lib() -> C.CDLL:
         "hko_post_process": (None, [vp, vp, vp]),
         "hko_sample_texture": (None, [vp, u32, vp, u32, vp]),
         "hko_hash": (u32, [u32]),
+        "hko_unpack_fast_mismatches": (u32, []),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

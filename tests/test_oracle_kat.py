@@ -349,3 +349,24 @@ def test_integer_pow_accuracy_and_domain():
         assert math.isnan(L.hko_pow_int(-1.0, n)) and math.isnan(L.hko_pow_int(float("nan"), n))
         assert math.copysign(1.0, L.hko_pow_int(-0.0, n)) == 1.0 and L.hko_pow_int(0.0, n) == 0.0
         assert L.hko_pow_int(float("inf"), n) == float("inf")
+
+
+def test_divide_free_unorm16_snorm8_decodes_are_exact(oracle_lib):
+    """hk_unpack_unorm16_fast / hk_unpack_snorm8_fast (device kernels: x * RN(1/d) plus one residual
+    correction) equal unpack2x16unorm / unpack4x8snorm's divisions for every code: compiled (host C,
+    hko_unpack_fast_mismatches) and as a formula in exact rational arithmetic."""
+    from fractions import Fraction as Fr
+    assert oracle_lib.hko_unpack_fast_mismatches() == 0
+
+    def rn(x):  # exact rational -> nearest f32, ties to even
+        a = np.float32(float(x))
+        c = [np.nextafter(a, np.float32(-np.inf)), a, np.nextafter(a, np.float32(np.inf))]
+        return min(c, key=lambda v: (abs(Fr(float(v)) - x), int(np.float32(v).view(np.uint32)) & 1))
+
+    for d, codes in ((65535, range(0, 65536, 7)), (127, range(-128, 128))):
+        r = rn(Fr(1, d))
+        for v in codes:
+            q0 = rn(Fr(v) * Fr(float(r)))
+            e = rn(Fr(float(-q0)) * d + v)
+            q1 = rn(Fr(float(e)) * Fr(float(r)) + Fr(float(q0)))
+            assert q1 == rn(Fr(v, d)), (d, v)

@@ -5,7 +5,13 @@ and runs the bench workload on it; the slowest band's ms/frame is the per-GPU co
 the N-GPU frame (the RCCL all-gather of frame f overlaps frame f+1 in bench.py).  This projects
 the strong-scaling curve when no multi-GPU box is at hand; it is not a multi-GPU measurement.
 Frames without neighbour reads use bench.py's interleaved stripes (--bands: contiguous bands).
-usage: python tools/band_scaling.py [config] [steps] [--bands]"""
+
+The projection adds the collective: one all-gather of the tone-mapped RGBA16F frame
+(8 B/px) per displayed frame, whose ring moves (N-1)/N of the frame through each GPU's busiest xGMI
+link at ~153 GB/s (MI355X: 7 links x ~153 GB/s per GPU).  bench.py double-buffers it, so the gather of
+frame f runs on RCCL's stream next to frame f+1: frame time = max(compute, gather) when it overlaps,
+compute + gather when it does not; both are printed.
+usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N]"""
 import json
 import sys
 import time
@@ -30,8 +36,19 @@ st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spa
 s = st.to_c()
 torch.cuda.set_device(0)
 sp = torch.cuda.current_stream().cuda_stream
-out = {"config": cfg_name, "resolution": [W, H], "bands": {}}
+XGMI_LINK_GBS = 153.0  # one xGMI link, GB/s per direction
+
+
+def allgather_ms(n: int) -> float:
+    """Ring all-gather of the W x H RGBA16F frame over N GPUs, bound by one link: (N-1)/N x 8 B/px."""
+    return 0.0 if n == 1 else (n - 1) / n * W * H * 8 / (XGMI_LINK_GBS * 1e9) * 1e3
+
+
+out = {"config": cfg_name, "resolution": [W, H], "bands": {}, "allgather_ms": {}, "projected_ms": {}}
+only = int(sys.argv[sys.argv.index("--only") + 1]) if "--only" in sys.argv else None
 for n in (1, 2, 4, 8):
+    if only is not None and n != only:
+        continue
     worst = 0.0
     stripes = use_stripes(cfg["spatial"], cfg["denoise"]) and "--bands" not in sys.argv
     for rank in sorted({0, n // 2, n - 1}):  # edge and middle bands
@@ -76,5 +93,10 @@ for n in (1, 2, 4, 8):
             r.enable_kernel_timing(False)
         r.close()
     out["bands"][n] = round(worst, 4)
-    print(f"N={n}: slowest band {worst:.4f} ms/frame  (projected speedup {out['bands'][1] / worst:.2f}x)", flush=True)
+    g = allgather_ms(n)
+    out["allgather_ms"][n] = round(g, 4)
+    out["projected_ms"][n] = {"overlapped": round(max(worst, g), 4), "serial": round(worst + g, 4)}
+    base = out["bands"].get(1)
+    speedup = f"  speedup {base / max(worst, g):.2f}x overlapped, {base / (worst + g):.2f}x serial" if base else ""
+    print(f"N={n}: slowest band {worst:.4f} ms/frame, all-gather {g:.4f} ms{speedup}", flush=True)
 print(json.dumps(out))
