@@ -1415,8 +1415,8 @@ HKD f4 noise_random(const uchar4* noise, uint32_t number, int32_t x, int32_t y)
     uint32_t tx = ((uint32_t)x + number) & 63u, ty = ((uint32_t)y + number) & 63u;
     uchar4 t = noise[(id * 64u + ty) * 64u + tx];
     float fn = (float)number * HK_GOLDEN_RATIO;
-    return mk4(hk_fract((float)t.x / 255.0f + fn), hk_fract((float)t.y / 255.0f + fn), hk_fract((float)t.z / 255.0f + fn),
-               hk_fract((float)t.w / 255.0f + fn));
+    return mk4(hk_fract(hk_unorm8_fast(t.x) + fn), hk_fract(hk_unorm8_fast(t.y) + fn), hk_fract(hk_unorm8_fast(t.z) + fn),
+               hk_fract(hk_unorm8_fast(t.w) + fn));
 }
 
 // Ray counters are sharded: COUNTER_SHARDS 64-byte lines per counter, each wave adds its

@@ -25,9 +25,10 @@ assert RESERVOIR_DTYPE.itemsize == 64
 
 
 def _stream(stream):
-    """A hipStream_t handle for the C ABI: None (the context's own stream) or an integer address
-    (e.g. torch.cuda.Stream.cuda_stream); anything else is refused here, before it reaches HIP."""
-    if stream is None or isinstance(stream, int):
+    """A hipStream_t handle for the C ABI: None (the context's own stream), an integer address (e.g.
+    torch.cuda.Stream.cuda_stream) or a ctypes.c_void_p; anything else is refused here, before it
+    reaches HIP."""
+    if stream is None or isinstance(stream, (int, C.c_void_p)):
         return stream
     raise TypeError(f"stream must be None or an integer hipStream_t handle, not {type(stream).__name__}")
 

@@ -238,16 +238,24 @@ HK_HD float hk_unpack_snorm8(uint32_t v, int c)
 
 /* The same two decodes without the divide, for the device kernels (the oracle keeps the divisions
  * above as its restatement): q0 = v * RN(1/d) and one residual correction give RN(v / d) for every
- * input of these integer domains — all 65,536 unorm16 and all 256 snorm8 codes, checked exhaustively
+ * input of these integer domains — all 65,536 unorm16 and all 256 snorm8 / unorm8 codes, checked exhaustively
  * by hko_unpack_fast_mismatches (tests/test_oracle_kat.py) and, for the formula itself, in exact
  * rational arithmetic.  3 instructions instead of the IEEE divide sequence. */
 #define HK_INV_65535 0x1.00010p-16f /* RN(1 / 65535) */
 #define HK_INV_127 0x1.020408p-7f   /* RN(1 / 127) */
+#define HK_INV_255 0x1.010102p-8f   /* RN(1 / 255) */
 HK_HD float hk_unpack_unorm16_fast(uint32_t v)
 {
     const float x = (float)(v & 0xFFFFu);
     const float q = x * HK_INV_65535;
     return fmaf(fmaf(-q, 65535.0f, x), HK_INV_65535, q);
+}
+/* f32(byte) / 255 (an RGBA8 unorm texel, e.g. the blue noise) the same way: exact for all 256 codes */
+HK_HD float hk_unorm8_fast(uint32_t byte)
+{
+    const float x = (float)(byte & 0xFFu);
+    const float q = x * HK_INV_255;
+    return fmaf(fmaf(-q, 255.0f, x), HK_INV_255, q);
 }
 HK_HD float hk_unpack_snorm8_fast(uint32_t v, int c)
 {

@@ -2393,8 +2393,10 @@ uint32_t hko_unpack_fast_mismatches(void)
     uint32_t bad = 0;
     for (uint32_t v = 0; v < 65536u; ++v)
         if (hk_f2u(hk_unpack_unorm16_fast(v)) != hk_f2u(hk_unpack_unorm16(v))) ++bad;
-    for (uint32_t v = 0; v < 256u; ++v)
+    for (uint32_t v = 0; v < 256u; ++v) {
         if (hk_f2u(hk_unpack_snorm8_fast(v << 8, 1)) != hk_f2u(hk_unpack_snorm8(v << 8, 1))) ++bad;
+        if (hk_f2u(hk_unorm8_fast(v)) != hk_f2u((float)v / 255.0f)) ++bad;
+    }
     return bad;
 }
 float hko_pow(float x, float y) { return hk_pow(x, y); }

@@ -352,8 +352,9 @@ def test_integer_pow_accuracy_and_domain():
 
 
 def test_divide_free_unorm16_snorm8_decodes_are_exact(oracle_lib):
-    """hk_unpack_unorm16_fast / hk_unpack_snorm8_fast (device kernels: x * RN(1/d) plus one residual
-    correction) equal unpack2x16unorm / unpack4x8snorm's divisions for every code: compiled (host C,
+    """hk_unpack_unorm16_fast / hk_unpack_snorm8_fast / hk_unorm8_fast (device kernels: x * RN(1/d) plus
+    one residual correction) equal unpack2x16unorm / unpack4x8snorm / the RGBA8 texel's divisions for every
+    code: compiled (host C,
     hko_unpack_fast_mismatches) and as a formula in exact rational arithmetic."""
     from fractions import Fraction as Fr
     assert oracle_lib.hko_unpack_fast_mismatches() == 0
@@ -363,7 +364,7 @@ def test_divide_free_unorm16_snorm8_decodes_are_exact(oracle_lib):
         c = [np.nextafter(a, np.float32(-np.inf)), a, np.nextafter(a, np.float32(np.inf))]
         return min(c, key=lambda v: (abs(Fr(float(v)) - x), int(np.float32(v).view(np.uint32)) & 1))
 
-    for d, codes in ((65535, range(0, 65536, 7)), (127, range(-128, 128))):
+    for d, codes in ((65535, range(0, 65536, 7)), (127, range(-128, 128)), (255, range(256))):
         r = rn(Fr(1, d))
         for v in codes:
             q0 = rn(Fr(v) * Fr(float(r)))
