@@ -489,6 +489,38 @@ HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
     p[res_chunk(b, 3, u)] = c3;
 }
 
+// Spatial view planes (ChannelArgs::view): spatial reuse reads a neighbour's record for its rejection
+// tests and its merge only (light.wgsl:1598-1642), so the temporal pass also stores, from the same packed
+// words it writes into `cur`:
+//   plane 0: sample_position xyz (c2.xyz) | the visible normal's snorm8 bytes (c3.x bits 0-23), bit 24:
+//            q.s.sample_position.w > 0.5 (the jacobian's condition, c3.y byte 3), bit 25: !(q.count < eps)
+//   plane 1: radiance (c0.xy, f16 x 4) | (count, w) (c3.z) | fract(dot(random, 1)) of the packed random
+//            (c0.zw decoded), the value update_reservoir compares (light.wgsl:155)
+//   plane 2: visible_position xyz (c1.xyz) | the sample normal's snorm8 word (c3.y)
+// Every field is the bits, or the exact value, spatial reuse would derive from the packed record, so the
+// results are unchanged; a tested neighbour costs one 16-B gather instead of two and a merged one two or
+// three instead of four.
+constexpr uint32_t VIEW_HIT = 1u << 24, VIEW_COUNT = 1u << 25;
+HKD void store_res_view(const ResBuf& b, uint4* view, uint32_t view_n, int32_t i, const Reservoir& r)
+{
+    uint4 c0, c1, c2, c3;
+    pack_res(r, c0, c1, c2, c3);
+    uint4* p = b.base;
+    const uint32_t u = (uint32_t)i;
+    p[res_chunk(b, 0, u)] = c0;
+    p[res_chunk(b, 1, u)] = c1;
+    p[res_chunk(b, 2, u)] = c2;
+    p[res_chunk(b, 3, u)] = c3;
+    if (!view) return;
+    const uint32_t flags = (hk_unpack_snorm8_fast(c3.y, 3) > 0.5f ? VIEW_HIT : 0u) |
+                           (!(unpack_lo16float(c3.z) < HK_F32_EPSILON) ? VIEW_COUNT : 0u);
+    const float rand = hk_fract(((hk_unpack_unorm16_fast(c0.z) + hk_unpack_unorm16_fast(c0.z >> 16)) +
+                                 hk_unpack_unorm16_fast(c0.w)) + hk_unpack_unorm16_fast(c0.w >> 16));
+    view[u] = make_uint4(c2.x, c2.y, c2.z, (c3.x & 0x00FFFFFFu) | flags);
+    view[view_n + u] = make_uint4(c0.x, c0.y, c3.z, __float_as_uint(rand));
+    view[2u * view_n + u] = make_uint4(c1.x, c1.y, c1.z, c3.y);
+}
+
 HKD void set_reservoir(Reservoir& r, const Sample& s, float w_new)
 {
     r.count = 1.0f;

@@ -897,7 +897,7 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
     r.s.visible_normal = s.visible_normal;
     r.lifetime += 1.0f;
     C.variance[idx] = variance_of(r);
-    if (F.temporal_reuse > 0u) store_res(C.cur, idx, r);
+    if (F.temporal_reuse > 0u) store_res_view(C.cur, C.view, C.view_n, idx, r);
     f3 o = out * r.w;
     store_rgba16f(C.render, idx, mk4(o.x, o.y, o.z, 1.0f));
     return true;
@@ -1112,7 +1112,7 @@ HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t
 // carried sample (plus the copy per merge) leave the loop.
 constexpr int32_t SEL_OWN = -1, SEL_PREVIOUS = -2;
 
-template <bool EMISSIVE_LIT, bool WINDOW>
+template <bool EMISSIVE_LIT, bool WINDOW, bool VIEW>
 HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32_t y, const DepthWin& W)
 {
     const Frame& F = A.F;
@@ -1167,19 +1167,19 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     f3 view_direction = calculate_view(F, position);
     const ShadeCtx sc = shade_ctx(F, view_direction, s.visible_normal, surface);
     // merge_reservoir(r, own, p) (light.wgsl:153-160)
-    auto merge = [&](float p, float q_w, float q_count, f4 q_random, int32_t q_sel) {
+    // rand: fract(dot(q.s.random, 1)), the value update_reservoir compares (light.wgsl:155)
+    auto merge = [&](float p, float q_w, float q_count, float rand, int32_t q_sel) {
         const float w_new = (p * q_w) * q_count;
         r_w_sum += w_new;
         r_w2_sum += w_new * w_new;
-        const float rand = hk_fract(sum4(q_random));
         if (rand < w_new / r_w_sum) sel = q_sel;
         r_count = r_count + q_count;
     };
     if (EMISSIVE_LIT) {
-        merge(lum(xyz(s.radiance)), own.w, own.count, s.random, SEL_OWN);
+        merge(lum(xyz(s.radiance)), own.w, own.count, hk_fract(sum4(s.random)), SEL_OWN);
     } else {
         f3 o = shade(sc, normalize(xyz(s.sample_position) - xyz(s.visible_position)), s.radiance);
-        merge(lum(o), own.w, own.count, s.random, SEL_OWN);
+        merge(lum(o), own.w, own.count, hk_fract(sum4(s.random)), SEL_OWN);
     }
 
     const float rf = hk_random_float(F.number);
@@ -1255,13 +1255,31 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         // tests read plane 3 (count, normals) and plane 2 (sample position); planes 0-1 only for a
         // neighbour that is merged): the same values as load_res, fewer gathers for rejected ones
         const int32_t nidx = s_index(F, scx, scy);
-        const uint4 c3 = C.cur.base[res_chunk(C.cur, 3u, (uint32_t)nidx)];
-        const float q_count = unpack_lo16float(c3.z);
-        const f3 q_normal = normalize(mk3(hk_unpack_snorm8_fast(c3.x, 0), hk_unpack_snorm8_fast(c3.x, 1), hk_unpack_snorm8_fast(c3.x, 2)));
+        // the neighbour's record: the view planes (VIEW, store_res_view) or the reservoir's own 16-byte
+        // planes, loaded as the tests need them (rejection: plane 3 count / normal, plane 2 sample
+        // position; merge: planes 0-1): the same values as load_res either way
+        uint4 c3 = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t normal_word;
+        bool count_ok;
+        f3 q_sample;
+        if constexpr (VIEW) {
+            const uint4 a = C.view[nidx];
+            normal_word = a.w;
+            count_ok = (a.w & VIEW_COUNT) != 0u;
+            q_sample = mk3(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
+        } else {
+            c3 = C.cur.base[res_chunk(C.cur, 3u, (uint32_t)nidx)];
+            normal_word = c3.x;
+            count_ok = !(unpack_lo16float(c3.z) < HK_F32_EPSILON);
+        }
+        const f3 q_normal = normalize(mk3(hk_unpack_snorm8_fast(normal_word, 0), hk_unpack_snorm8_fast(normal_word, 1),
+                                          hk_unpack_snorm8_fast(normal_word, 2)));
         bool normal_miss = dot(s_normal, q_normal) < 0.866f;
-        if (q_count < HK_F32_EPSILON || normal_miss) continue;
-        const uint4 c2 = C.cur.base[res_chunk(C.cur, 2u, (uint32_t)nidx)];
-        const f3 q_sample = mk3(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z));
+        if (!count_ok || normal_miss) continue;
+        if constexpr (!VIEW) {
+            const uint4 c2 = C.cur.base[res_chunk(C.cur, 2u, (uint32_t)nidx)];
+            q_sample = mk3(__uint_as_float(c2.x), __uint_as_float(c2.y), __uint_as_float(c2.z));
+        }
         // normalize(q_sample - visible), its length kept for the jacobian below
         const f3 to_sample = q_sample - s_visible;
         const float to_sample_length = sqrtf(dot(to_sample, to_sample));
@@ -1269,20 +1287,42 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         if (dot(sample_direction, s_normal) < 0.0f) continue;
 
         // merge_reservoir(r, q, p / jacobian): the fields of q that the merge reads
-        const uint4 c0 = C.cur.base[res_chunk(C.cur, 0u, (uint32_t)nidx)];
-        const float q_w = unpack_hi16float(c3.z);
-        const f4 q_radiance = mk4(unpack_lo16float(c0.x), unpack_hi16float(c0.x), unpack_lo16float(c0.y),
-                                  unpack_hi16float(c0.y));
-        const f4 q_random = mk4(hk_unpack_unorm16_fast(c0.z), hk_unpack_unorm16_fast(c0.z >> 16), hk_unpack_unorm16_fast(c0.w),
-                                hk_unpack_unorm16_fast(c0.w >> 16));
+        float q_w, q_count, q_rand;
+        f4 q_radiance;
+        bool hit;
+        if constexpr (VIEW) {
+            const uint4 b = C.view[C.view_n + (uint32_t)nidx];
+            q_radiance = mk4(unpack_lo16float(b.x), unpack_hi16float(b.x), unpack_lo16float(b.y), unpack_hi16float(b.y));
+            q_count = unpack_lo16float(b.z);
+            q_w = unpack_hi16float(b.z);
+            q_rand = __uint_as_float(b.w);
+            hit = (normal_word & VIEW_HIT) != 0u;
+        } else {
+            const uint4 c0 = C.cur.base[res_chunk(C.cur, 0u, (uint32_t)nidx)];
+            q_radiance = mk4(unpack_lo16float(c0.x), unpack_hi16float(c0.x), unpack_lo16float(c0.y), unpack_hi16float(c0.y));
+            q_count = unpack_lo16float(c3.z);
+            q_w = unpack_hi16float(c3.z);
+            q_rand = hk_fract(sum4(mk4(hk_unpack_unorm16_fast(c0.z), hk_unpack_unorm16_fast(c0.z >> 16),
+                                       hk_unpack_unorm16_fast(c0.w), hk_unpack_unorm16_fast(c0.w >> 16))));
+            hit = hk_unpack_snorm8_fast(c3.y, 3) > 0.5f;
+        }
         float jacobian = 1.0f;
-        if (hk_unpack_snorm8_fast(c3.y, 3) > 0.5f) {
+        if (hit) {
             // compute_jacobian(q.s, s) (light.wgsl:990-1004).  Its first vector, visible - q_sample,
             // is -to_sample exactly, so its normalisation is -sample_direction and its length is
             // to_sample_length, bit for bit (negation is exact; the squares are equal)
-            const uint4 c1 = C.cur.base[res_chunk(C.cur, 1u, (uint32_t)nidx)];
+            uint4 c1;
+            uint32_t sample_normal_word;
+            if constexpr (VIEW) {
+                c1 = C.view[2u * C.view_n + (uint32_t)nidx];
+                sample_normal_word = c1.w;
+            } else {
+                c1 = C.cur.base[res_chunk(C.cur, 1u, (uint32_t)nidx)];
+                sample_normal_word = c3.y;
+            }
             const f3 q_visible = mk3(__uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z));
-            const f3 normal = normalize(mk3(hk_unpack_snorm8_fast(c3.y, 0), hk_unpack_snorm8_fast(c3.y, 1), hk_unpack_snorm8_fast(c3.y, 2)));
+            const f3 normal = normalize(mk3(hk_unpack_snorm8_fast(sample_normal_word, 0), hk_unpack_snorm8_fast(sample_normal_word, 1),
+                                            hk_unpack_snorm8_fast(sample_normal_word, 2)));
             const float c1_ = fabsf(dot(sample_direction, normal));
             const f3 back = q_visible - q_sample;
             const float back_length = sqrtf(dot(back, back));
@@ -1294,10 +1334,10 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             jacobian = hk_clampf(term_1 * term_2, 1.0f, 50.0f);
         }
         if (EMISSIVE_LIT) {
-            merge(lum(xyz(q_radiance)) / jacobian, q_w, q_count, q_random, nidx);
+            merge(lum(xyz(q_radiance)) / jacobian, q_w, q_count, q_rand, nidx);
         } else {
             f3 o = shade(sc, sample_direction, q_radiance);
-            merge(lum(o) / jacobian, q_w, q_count, q_random, nidx);
+            merge(lum(o) / jacobian, q_w, q_count, q_rand, nidx);
         }
     }
     // the selected sample, re-read from its record (see SEL_OWN above)
@@ -1339,7 +1379,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     store_rgba16f(C.render, idx, mk4(oc.x, oc.y, oc.z, 1.0f));
 }
 
-template <bool EMISSIVE_LIT, bool WINDOW>
+template <bool EMISSIVE_LIT, bool WINDOW, bool VIEW>
 __global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, ChannelArgs C)
 {
     __shared__ float win[WINDOW ? SP_WIN * SP_WIN : 1];
@@ -1355,7 +1395,7 @@ __global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, Cha
         W.lds = win;
     }
     int32_t x, y;
-    if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT, WINDOW>(A, C, x, y, W);
+    if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT, WINDOW, VIEW>(A, C, x, y, W);
 }
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
@@ -1682,12 +1722,16 @@ void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit,
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     // the window assumes integrator pixels == deferred pixels (upscale ratio 1)
     const bool window = A.F.upscale_ratio == 1.0f && A.F.s[0] == A.F.S[0] && A.F.s[1] == A.F.S[1];
+    // the view planes hold the indirect channel's records only (ChannelArgs::view)
     if (emissive_lit) {
-        if (window) hipLaunchKernelGGL((k_spatial<true, true>), g, dim3(256), 0, st, A, C);
-        else hipLaunchKernelGGL((k_spatial<true, false>), g, dim3(256), 0, st, A, C);
+        if (window) hipLaunchKernelGGL((k_spatial<true, true, false>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial<true, false, false>), g, dim3(256), 0, st, A, C);
+    } else if (C.view) {
+        if (window) hipLaunchKernelGGL((k_spatial<false, true, true>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial<false, false, true>), g, dim3(256), 0, st, A, C);
     } else {
-        if (window) hipLaunchKernelGGL((k_spatial<false, true>), g, dim3(256), 0, st, A, C);
-        else hipLaunchKernelGGL((k_spatial<false, false>), g, dim3(256), 0, st, A, C);
+        if (window) hipLaunchKernelGGL((k_spatial<false, true, false>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial<false, false, false>), g, dim3(256), 0, st, A, C);
     }
 }
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)

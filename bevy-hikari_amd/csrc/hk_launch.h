@@ -33,6 +33,12 @@ struct ChannelArgs {
     // stores target; when all are set the stores are skipped (same bits in every buffer).
     uint8_t* bg;
     uint32_t bg_need;
+    // Spatial view planes (indirect channel; nullptr elsewhere): 3 planes of view_n 16-byte chunks holding
+    // what spatial reuse reads from a NEIGHBOUR's temporal record, derived from the packed words this
+    // frame's temporal pass stores into `cur` (store_res_view, hk_device.h).  Written by the indirect
+    // temporal pass when non-null, read by k_spatial<false, ·, true>.
+    uint4* view;
+    uint32_t view_n;
 };
 
 // Wavefront indirect pass (config 5: material-sorted shading), see hk_kernels.hip k_wf_*.

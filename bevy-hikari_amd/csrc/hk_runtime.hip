@@ -129,6 +129,7 @@ struct hk_ctx {
     bool bg_valid[2] = {false, false};
     int32_t bg_key[2][2] = {};
     uint8_t* gbmask = nullptr;  // the G-buffer's (ViewArgs::bg), per S pixel
+    uint4* sp_view = nullptr;   // spatial view planes of the indirect channel (ChannelArgs::view), 3 x res_n
     bool gb_valid = false;
     int32_t gb_key[2] = {};
     // denoise
@@ -279,6 +280,7 @@ void free_targets(hk_ctx* c)
     }
     release(c->gbmask);
     c->gb_valid = false;
+    release(c->sp_view);
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) release(c->internal[ch][i]);
         release(c->internal_variance[ch]);
@@ -1060,6 +1062,8 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     }
     HK_HIP(c, hipMalloc(&c->gbmask, SP));
     c->gb_valid = false;
+    HK_HIP(c, hipMalloc(&c->sp_view, 3 * sp * sizeof(uint4)));
+    HK_HIP(c, hipMemset(c->sp_view, 0, 3 * sp * sizeof(uint4)));
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) {
             HK_HIP(c, hipMalloc(&c->internal[ch][i], sp * sizeof(uint2)));
@@ -1239,6 +1243,8 @@ static ChannelArgs channel(hk_ctx* c, uint32_t number, int ch)
     ChannelArgs C;
     C.bg = nullptr;
     C.bg_need = 0;
+    C.view = nullptr;
+    C.view_n = 0;
     C.prev = ResBuf{c->reservoirs[current + pairs[ch][0]], c->res_n};
     C.cur = ResBuf{c->reservoirs[previous + pairs[ch][0]], c->res_n};
     C.prev_spatial = ResBuf{c->reservoirs[current + pairs[ch][1]], c->res_n};
@@ -1351,6 +1357,15 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     }
     if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(AS, C1, true, s1); });
     ChannelArgs C2 = channel(c, A.F.number, 2);
+    // spatial view planes (ChannelArgs::view): the indirect temporal pass writes them next to the records
+    // it stores, this frame's spatial pass reads its neighbours from them.  Only when that temporal pass
+    // stores its records (temporal_reuse; otherwise `cur` keeps older records the planes do not mirror).
+    // HK_NO_SP_VIEW=1: off (the spatial pass gathers the records' own planes).
+    const char* nv = getenv("HK_NO_SP_VIEW");
+    if (settings->indirect_spatial_reuse && settings->temporal_reuse && !(nv && nv[0] == '1')) {
+        C2.view = c->sp_view;
+        C2.view_n = c->res_n;
+    }
     bool multi = settings->indirect_bounces >= 2u;
     // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
     const bool wf = c->wavefront && !multi && c->count[6] + 1u <= WF_MAX_BINS;

@@ -667,3 +667,30 @@ def test_post_process_smaa_taa_bit_exact(ratio_setting, taa, pipelined, monkeypa
         for oid in outs:
             m = mismatch_report(canon_plane(10, r.output(oid)), canon_plane(10, o.output(oid)), f"frame {f} output {oid}")
             assert not m, m
+
+
+@pytest.mark.parametrize("mode", ["no_view", "no_temporal_reuse"])
+def test_spatial_reuse_without_view_planes_bit_exact(monkeypatch, mode):
+    """Spatial reuse gathering the neighbours' own reservoir planes instead of the spatial view planes
+    (hk_device.h store_res_view): forced with HK_NO_SP_VIEW=1, and taken by the runtime when the temporal
+    pass does not store its records (temporal_reuse = false: the records in `cur` are older than any view
+    plane).  Every plane and reservoir bit-exact against the oracle over 6 frames."""
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    if mode == "no_view":
+        monkeypatch.setenv("HK_NO_SP_VIEW", "1")
+    w, h = 64, 64
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, temporal_reuse=mode != "no_temporal_reuse")
+    scene, cam, lights, r, o = _setup(w, h, st)
+    s = st.to_c()
+    errors = []
+    for f in range(6):
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        _compare_frame(r, o, f, errors)
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
