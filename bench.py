@@ -57,6 +57,7 @@ BYTES_PER_PIXEL = {
     "direct_lit": (184, 92),
     "direct_emissive": (184, 220),
     "direct_lit_emissive": (324, 296),  # both passes in one launch (k_direct_fused): the G-buffer read once
+    "light_merged": (508, 516),          # k_light_merged: direct_lit_emissive + indirect_lit_ambient
     "indirect_lit_ambient": (184, 220),
     "indirect_multiple_bounces": (184, 220),
     "indirect_wavefront": (184, 220),    # the same compulsory streams (queues / hit records are extra traffic)
@@ -85,6 +86,9 @@ BG_ELIDED_BYTES = {"gbuffer": (None, 1, 1),  # a miss: its mask byte (the slot a
 
 
 def kernel_bytes(name: str, covered_px: float, background_px: float, settings=None) -> float:
+    if name == "light_merged":  # k_light_merged: the fused direct/emissive pass and the indirect pass in one launch
+        return (kernel_bytes("direct_lit_emissive", covered_px, background_px, settings) +
+                kernel_bytes("indirect_lit_ambient", covered_px, background_px, settings))
     c, b = BYTES_PER_PIXEL.get(name, (0, 0))
     if settings is not None and name in BG_ELIDED_BYTES and os.environ.get("HK_NO_BG_ELIDE") != "1":
         flag, alone, with_pair = BG_ELIDED_BYTES[name]

@@ -57,13 +57,12 @@ enum TileOrder : int { RASTER = 0, XCD_RASTER = 1, XCD_STRIPS = 2 };
 #endif
 constexpr uint32_t STRIP_TILES = HK_STRIP_TILES;
 template <int ORDER>
-HKD void tile_coords(uint32_t& tx, uint32_t& ty)
+HKD void tile_coords_at(uint32_t bx, uint32_t by, uint32_t gx, uint32_t gy, uint32_t& tx, uint32_t& ty)
 {
-    const uint32_t gx = gridDim.x, gy = gridDim.y;
-    const uint32_t L = blockIdx.x + blockIdx.y * gx;
+    const uint32_t L = bx + by * gx;
     if (ORDER == RASTER) {
-        tx = blockIdx.x;
-        ty = blockIdx.y;
+        tx = bx;
+        ty = by;
         return;
     }
     const uint32_t n = gx * gy;
@@ -80,11 +79,18 @@ HKD void tile_coords(uint32_t& tx, uint32_t& ty)
     ty = k / sw;
     tx = strip * STRIP_TILES + (k - ty * sw);
 }
+template <int ORDER>
+HKD void tile_coords(uint32_t& tx, uint32_t& ty)
+{
+    tile_coords_at<ORDER>(blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, tx, ty);
+}
+// the pixel of this thread in tile (bx, by) of a gx x gy tile grid (tile_pixel: the launch's own grid)
 template <int ORDER = RASTER>
-HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
+HKD bool tile_pixel_at(const Frame& F, uint32_t width, int32_t row0, int32_t rows, uint32_t bx, uint32_t by, uint32_t gx,
+                       uint32_t gy, int32_t& x, int32_t& y)
 {
     uint32_t tx, ty;
-    tile_coords<ORDER>(tx, ty);
+    tile_coords_at<ORDER>(bx, by, gx, gy, tx, ty);
     uint32_t t = threadIdx.x;
     uint32_t w = t >> 6, lane = t & 63u;
     x = (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
@@ -93,6 +99,11 @@ HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, 
     int32_t ly = w0 + (int32_t)(ty * 16u + (w >> 1) * 8u + (lane >> 3));
     y = global_row(F, ly, row0);
     return (uint32_t)x < width && ly < w1;
+}
+template <int ORDER = RASTER>
+HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
+{
+    return tile_pixel_at<ORDER>(F, width, row0, rows, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, x, y);
 }
 
 // Occupancy hints for the traversal kernels (waves per SIMD); tunable at build time.
@@ -389,7 +400,9 @@ HKD float* park_area()
     return park;
 }
 
-template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, bool PARK = false>
+// PARK: 0 = the validation block keeps the reservoir in registers, 1 = parks it in a static LDS array,
+// 2 = in the launch's dynamic LDS (k_light_merged: the direct and indirect workgroups share one buffer)
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, int PARK = 0>
 HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel P, uint32_t& n_top,
                      uint32_t& n_emitter, Surface* surface_out = nullptr, const Surface* surface_in = nullptr)
 {
@@ -465,7 +478,7 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     if (VALIDATE && umod(F.number, validate_interval) == 0u) {
         float* lds = nullptr;
         if constexpr (PARK) {
-            lds = park_area();
+            lds = PARK == 2 ? reinterpret_cast<float*>(hk_lds_scene) : park_area();
             park_sample(lds, s);
             park_reservoir(lds, r);
         }
@@ -914,6 +927,46 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
     }
     uint32_t n_top = 0, n_emitter = 0;
     if (active) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
+// The fused direct/emissive pass and the one-bounce indirect pass in ONE launch.  They read the same
+// G-buffer and write disjoint buffers (reservoirs 0-5 and the direct / emissive planes, reservoirs 6-9
+// and the indirect planes: light.rs:518-546), so their workgroups are independent and are interleaved
+// in one grid — even blockIdx.x: a direct tile, odd: the indirect tile — instead of the indirect pass
+// running on a side stream joined by events.  Each CU then mixes both kinds of work and the frame has
+// no cross-stream dependency: cornell 8-way stripe ....  Same per-pixel code as
+// k_direct_fused_w4 / k_indirect, so the results are identical.  The direct role parks its validation
+// state in the dynamic LDS buffer the indirect role stages the scene into (PARK 2): one buffer of
+// max(park, scene) bytes per workgroup, as each kernel alone needs.
+template <bool VD, bool VE, bool LDS_I>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_light_merged(FrameArgs A, ChannelArgs C0,
+                                                                                                ChannelArgs C1, ChannelArgs C2)
+{
+    const uint32_t bx = blockIdx.x >> 1, gx = gridDim.x >> 1;
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    const bool active = tile_pixel_at<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, bx, blockIdx.y, gx, gridDim.y, x, y);
+    if (blockIdx.x & 1u) {
+        Scene sc = A.sc;
+        if constexpr (LDS_I) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+        if (active) indirect_body<false>(A, sc, C2, x, y, n_top, n_emitter);
+    } else if (active) {
+        const Scene& sc = A.sc;
+        const DirectPixel P = load_direct_pixel(A, x, y);
+        const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
+        if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
+            const Reservoir z = background_reservoir();
+            store_res(C1.spatial, P.idx, z);
+            store_res(C1.prev_spatial, P.idx, z);
+        } else if (bg == BG_STORE) {
+            Surface surface;
+            direct_body<false, true, VD, 2>(A, sc, C0, P, n_top, n_emitter, &surface);
+            direct_body<true, false, VE, 2>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
+        }
+    }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -1702,6 +1755,26 @@ void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipSt
         if (lds) hipLaunchKernelGGL((k_indirect<false, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_indirect<false, false>), g, dim3(256), 0, st, A, C);
     }
+}
+bool light_lds_direct(const FrameArgs& A) { return lds_plan_bytes(A, PLAN_LIGHT, false) != 0u; }
+void launch_light_merged(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, const ChannelArgs& C2,
+                         hipStream_t st)
+{
+    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
+    g.x *= 2u;  // even: direct tile, odd: indirect tile (k_light_merged)
+    const uint32_t scene = lds_plan_bytes(A, PLAN_LIGHT, true);
+    const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
+    const bool ve = validation_frame(A.F.number, A.F.emissive_validate_interval);
+    const uint32_t park = (vd || ve) ? (uint32_t)(PARK_WORDS * 256 * sizeof(float)) : 0u;
+    const uint32_t lds = scene > park ? scene : park;
+#define HK_MERGED(VD_, VE_)                                                                                         \
+    if (scene) hipLaunchKernelGGL((k_light_merged<VD_, VE_, true>), g, dim3(256), lds, st, A, C0, C1, C2);          \
+    else hipLaunchKernelGGL((k_light_merged<VD_, VE_, false>), g, dim3(256), lds, st, A, C0, C1, C2);
+    if (vd && ve) { HK_MERGED(true, true) }
+    else if (vd) { HK_MERGED(true, false) }
+    else if (ve) { HK_MERGED(false, true) }
+    else { HK_MERGED(false, false) }
+#undef HK_MERGED
 }
 void launch_indirect_wavefront(const FrameArgs& A, const ChannelArgs& C, const WfArgs& W, hipStream_t st)
 {

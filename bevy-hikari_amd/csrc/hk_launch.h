@@ -142,6 +142,11 @@ void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipSt
 // material, material-sorted shade; W.ctl must be zeroed on `st` before
 void launch_indirect_wavefront(const FrameArgs& A, const ChannelArgs& C, const WfArgs& W, hipStream_t st);
 void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st);
+// the direct-light passes stage the scene in LDS (HK_LDS_SCENE=2 with a small enough scene)
+bool light_lds_direct(const FrameArgs& A);
+// direct_lit + emissive (fused per pixel) and the one-bounce indirect pass in one launch (k_light_merged)
+void launch_light_merged(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, const ChannelArgs& C2,
+                         hipStream_t st);
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st);
 void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st);
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st);

@@ -1317,11 +1317,9 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // overlap.  HK_CHANNEL_STREAMS=0 restores the serial order.
     bool fork = true;
     if (const char* e = getenv("HK_CHANNEL_STREAMS")) fork = e[0] == '1';
+    // fork_events: the indirect chain really runs on the side stream (not when k_light_merged takes it)
+    bool fork_events = false;
     hipStream_t s1 = st, s2 = fork ? c->side[1] : st;
-    if (fork) {
-        HK_HIP(c, hipEventRecord(c->ev_fork, st));
-        HK_HIP(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
-    }
     const FrameArgs A_all = A;
     if (!c->albedo_fresh) {
         const FrameArgs AG = pass_window(c, A_all, GBUFFER_REACH);
@@ -1346,16 +1344,6 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // background elision under the identity reprojection (every store on the thread's own pixel);
     // the separate launches share the pair's mask (direct_pass)
     const bool identity = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f;
-    HK_TRY(bg_mask(c, 0, A, identity, !settings->emissive_spatial_reuse, st, C0));
-    C1.bg = C0.bg;
-    C1.bg_need = C0.bg_need;
-    if (fuse) {
-        timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(A, C0, C1, st); });
-    } else {
-        timed(c, "direct_lit", st, [&] { launch_direct(A, C0, false, st); });
-        timed(c, "direct_emissive", s1, [&] { launch_direct(A, C1, true, s1); });
-    }
-    if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(AS, C1, true, s1); });
     ChannelArgs C2 = channel(c, A.F.number, 2);
     // spatial view planes (ChannelArgs::view): the indirect temporal pass writes them next to the records
     // it stores, this frame's spatial pass reads its neighbours from them.  Only when that temporal pass
@@ -1369,19 +1357,57 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     bool multi = settings->indirect_bounces >= 2u;
     // the wavefront pipeline covers one bounce and scenes with up to WF_MAX_BINS - 1 materials
     const bool wf = c->wavefront && !multi && c->count[6] + 1u <= WF_MAX_BINS;
-    // (the wavefront pass elides in its generation stage, which classifies every pixel)
-    HK_TRY(bg_mask(c, 1, A, identity, !settings->indirect_spatial_reuse, s2, C2));
-    if (wf) {
-        HK_TRY(ensure_wavefront(c));
-        WfArgs W{c->wf_queue1, c->wf_keys, c->wf_queue2, c->wf_hit, c->wf_hit_t, c->wf_ctl, c->count[6] + 1u,
-                 c->wf_seg_cap};
-        HK_HIP(c, hipMemsetAsync(W.ctl, 0, (size_t)wf_ctl_words(W.bins) * 4, s2));
-        timed(c, "indirect_wavefront", s2, [&] { launch_indirect_wavefront(A, C2, W, s2); });
-    } else {
-        timed(c, multi ? "indirect_multiple_bounces" : "indirect_lit_ambient", s2, [&] { launch_indirect(A, C2, multi, s2); });
+    // direct_lit + emissive (fused per pixel) and the one-bounce indirect pass in ONE launch
+    // (k_light_merged), replacing the indirect side stream and its fork / join events.  It needs the
+    // fused launch's conditions (identity reprojection) and a direct pass that does not stage the scene.
+    // By default only on small frames without spatial reuse: there each kernel lasts about one wave
+    // lifetime and the events' latency is a fifth of the frame (cornell 8-way stripe 0.144 -> 0.121
+    // ms/frame); on larger frames the two streams overlap better (4-way stripe 0.173 vs 0.177, 1080p
+    // 0.474 vs 0.511, city 4K 6.25 vs 7.21: spatial reuse would wait for the direct pass).  Not in the
+    // isolated-kernel measurement mode (HK_CHANNEL_STREAMS=0).  HK_MERGE=1: whenever possible, 0: never.
+    const char* me = getenv("HK_MERGE");
+    const bool merge_possible = identity && fork && !multi && !wf && !light_lds_direct(A) && !getenv("HK_NO_FUSE");
+    const bool merge_default = (double)c->s[0] * (double)c->s_rows <= 4.0e5 && !settings->indirect_spatial_reuse &&
+                               !settings->emissive_spatial_reuse;
+    const bool merge = merge_possible && (me ? me[0] == '1' : merge_default);
+    if (fork && !merge) {
+        HK_HIP(c, hipEventRecord(c->ev_fork, st));
+        HK_HIP(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
+        fork_events = true;
     }
-    if (settings->indirect_spatial_reuse) timed(c, "indirect_spatial_reuse", s2, [&] { launch_spatial(AS, C2, false, s2); });
-    if (fork) {
+    HK_TRY(bg_mask(c, 0, A, identity, !settings->emissive_spatial_reuse, st, C0));
+    C1.bg = C0.bg;
+    C1.bg_need = C0.bg_need;
+    if (merge) {
+        // (the elision mask of the indirect channel is prepared on the launch stream)
+        HK_TRY(bg_mask(c, 1, A, identity, !settings->indirect_spatial_reuse, st, C2));
+        timed(c, "light_merged", st, [&] { launch_light_merged(A, C0, C1, C2, st); });
+        if (settings->emissive_spatial_reuse)
+            timed(c, "emissive_spatial_reuse", st, [&] { launch_spatial(AS, C1, true, st); });
+        if (settings->indirect_spatial_reuse)
+            timed(c, "indirect_spatial_reuse", st, [&] { launch_spatial(AS, C2, false, st); });
+    } else {
+        if (fuse) {
+            timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(A, C0, C1, st); });
+        } else {
+            timed(c, "direct_lit", st, [&] { launch_direct(A, C0, false, st); });
+            timed(c, "direct_emissive", s1, [&] { launch_direct(A, C1, true, s1); });
+        }
+        if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(AS, C1, true, s1); });
+        // (the wavefront pass elides in its generation stage, which classifies every pixel)
+        HK_TRY(bg_mask(c, 1, A, identity, !settings->indirect_spatial_reuse, s2, C2));
+        if (wf) {
+            HK_TRY(ensure_wavefront(c));
+            WfArgs W{c->wf_queue1, c->wf_keys, c->wf_queue2, c->wf_hit, c->wf_hit_t, c->wf_ctl, c->count[6] + 1u,
+                     c->wf_seg_cap};
+            HK_HIP(c, hipMemsetAsync(W.ctl, 0, (size_t)wf_ctl_words(W.bins) * 4, s2));
+            timed(c, "indirect_wavefront", s2, [&] { launch_indirect_wavefront(A, C2, W, s2); });
+        } else {
+            timed(c, multi ? "indirect_multiple_bounces" : "indirect_lit_ambient", s2, [&] { launch_indirect(A, C2, multi, s2); });
+        }
+        if (settings->indirect_spatial_reuse) timed(c, "indirect_spatial_reuse", s2, [&] { launch_spatial(AS, C2, false, s2); });
+    }
+    if (fork_events) {
         HK_HIP(c, hipEventRecord(c->ev_join[1], s2));
         HK_HIP(c, hipStreamWaitEvent(st, c->ev_join[1], 0));
     }

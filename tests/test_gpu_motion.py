@@ -289,14 +289,17 @@ def test_host_gbuffer_planes_bit_exact():
 @pytest.mark.parametrize("lds", ["0", "1"])
 def test_forced_kernel_variants_bit_exact(monkeypatch, lds):
     """Kernel variants the size thresholds normally pick only at large sizes, forced on a small
-    frame: k_direct_lit_w4 (4 waves per SIMD; HK_DIRECT_W4_MIN_PX=0 with HK_NO_FUSE) and the fused
-    direct+emissive launch (HK_FUSE_MIN_PX=0), each with and without LDS scene staging."""
+    frame: k_direct_lit_w4 (4 waves per SIMD; HK_DIRECT_W4_MIN_PX=0 with HK_NO_FUSE), the fused
+    direct+emissive launch next to the indirect side stream (HK_FUSE_MIN_PX=0, HK_MERGE=0) and the
+    merged direct+indirect launch (k_light_merged, HK_MERGE=1: the default only for small frames without
+    spatial reuse; here with spatial reuse after it), each with and without LDS scene staging."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     monkeypatch.setenv("HK_LDS_SCENE", lds)
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
     s = st.to_c()
-    for env in ({"HK_DIRECT_W4_MIN_PX": "0", "HK_NO_FUSE": "1"}, {"HK_FUSE_MIN_PX": "0"}):
+    for env in ({"HK_DIRECT_W4_MIN_PX": "0", "HK_NO_FUSE": "1"}, {"HK_FUSE_MIN_PX": "0", "HK_MERGE": "0"},
+                {"HK_MERGE": "1"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         scene, cam, lights, r, o = _pair("cornell", w, h, st, threads=0)
