@@ -517,8 +517,10 @@ HKD void store_res_view(const ResBuf& b, uint4* view, uint32_t view_n, int32_t i
     const float rand = hk_fract(((hk_unpack_unorm16_fast(c0.z) + hk_unpack_unorm16_fast(c0.z >> 16)) +
                                  hk_unpack_unorm16_fast(c0.w)) + hk_unpack_unorm16_fast(c0.w >> 16));
     view[u] = make_uint4(c2.x, c2.y, c2.z, (c3.x & 0x00FFFFFFu) | flags);
-    view[view_n + u] = make_uint4(c0.x, c0.y, c3.z, __float_as_uint(rand));
-    view[2u * view_n + u] = make_uint4(c1.x, c1.y, c1.z, c3.y);
+    // spatial reuse reads plane 1 only behind VIEW_COUNT and plane 2 only behind VIEW_HIT (plane 0 of the
+    // same frame), so a chunk whose flag is clear is never read and its store is skipped
+    if (flags & VIEW_COUNT) view[view_n + u] = make_uint4(c0.x, c0.y, c3.z, __float_as_uint(rand));
+    if (flags & VIEW_HIT) view[2u * view_n + u] = make_uint4(c1.x, c1.y, c1.z, c3.y);
 }
 
 HKD void set_reservoir(Reservoir& r, const Sample& s, float w_new)

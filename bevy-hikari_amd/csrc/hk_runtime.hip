@@ -90,12 +90,13 @@ struct hk_ctx {
     uint2* albedo_prev = nullptr;
     // G-buffer pipelining: k_gbuffer of frame f runs on gb_stream, next to frame f-1's light passes
     hipStream_t gb_stream = nullptr;
-    hipEvent_t ev_gb_done = nullptr;            // after the latest k_gbuffer launch (either stream)
-    hipEvent_t ev_gb_call[2] = {nullptr, nullptr};  // caller stream at the entry of the last two calls
+    hipEvent_t ev_gb_done = nullptr;            // after the latest k_gbuffer launch on gb_stream
+    hipEvent_t ev_gb_call[2] = {nullptr, nullptr};  // caller stream at the entry of the last two pipelined calls
     hipEvent_t ev_post = nullptr;               // after a post-process read of the previous slot
     bool gb_pending = false;                    // a k_gbuffer launch was made on gb_stream
     bool gb_serial = true;                      // the next k_gbuffer runs in caller-stream order
     bool post_pending = false;
+    bool gb_call_rec = false;                   // the last call recorded ev_gb_call (it was pipelined)
     uint32_t gb_calls = 0;
     // Frame-tail pipelining: the demodulation, a-trous levels and tone-sum of frame f run on
     // dn_stream next to frame f+1's light passes; render / variance are double-buffered for it.
@@ -299,6 +300,7 @@ void free_targets(hk_ctx* c)
     release(c->albedo_prev);
     c->gb_serial = true;
     c->gb_calls = 0;
+    c->gb_call_rec = false;
     c->rf_swapped = c->tail_open = false;
     c->rslot_rec[0] = c->rslot_rec[1] = c->gslot_rec[0] = c->gslot_rec[1] = false;
     c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
@@ -1118,13 +1120,18 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     // passes.  A scene / size / plane change since the last call serialises it instead.
     const char* gp = getenv("HK_GB_PIPELINE");
     const bool pipeline = !gp || gp[0] != '0';
+    // Event markers are recorded only on the pipelined path: each one between two kernels of a stream
+    // costs it ~6 us (cornell 8-way stripe, where the serial frame is 3 kernels), and the serial path
+    // has no other stream waiting on them.
     const uint32_t e = c->gb_calls & 1u;
-    HK_HIP(c, hipEventRecord(c->ev_gb_call[e], st));
     hipStream_t gs = st;
-    if (pipeline && pipeline_size(c) && !c->gb_serial && c->gb_calls > 0) {
+    const bool pipe = pipeline && pipeline_size(c) && !c->gb_serial && c->gb_calls > 0;
+    if (pipe) {
+        HK_HIP(c, hipEventRecord(c->ev_gb_call[e], st));
         gs = c->gb_stream;
-        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[e ^ 1u], 0));
-        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_done, 0));  // the previous k_gbuffer (if it ran on st)
+        // the caller stream at the previous call's entry; when that call was serial (its k_gbuffer ran
+        // on st, no record), the caller stream now.  The previous pipelined k_gbuffer is earlier on gs.
+        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[c->gb_call_rec ? e ^ 1u : e], 0));
         if (c->post_pending) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_post, 0));
         // frame f-2's denoise on dn_stream read that slot
         if (c->gslot_rec[c->gslot ^ 1u]) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gslot[c->gslot ^ 1u], 0));
@@ -1191,8 +1198,11 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
                                    sizeof(hk_instance), 64, c->count[4], hipMemcpyDeviceToDevice, gs));
         c->models_dirty = false;
     }
-    HK_HIP(c, hipEventRecord(c->ev_gb_done, gs));
-    if (gs != st) c->gb_pending = true;
+    if (gs != st) {
+        HK_HIP(c, hipEventRecord(c->ev_gb_done, gs));
+        c->gb_pending = true;
+    }
+    c->gb_call_rec = pipe;
     c->gb_serial = false;
     c->gb_calls++;
     c->albedo_fresh = true;
