@@ -98,6 +98,16 @@ struct hk_ctx {
     bool post_pending = false;
     bool gb_call_rec = false;                   // the last call recorded ev_gb_call (it was pipelined)
     uint32_t gb_calls = 0;
+    // fork shortcut bookkeeping (pick / pick_frame, hk_render_frame): API calls outside the frame
+    // sequence, the frame sequence's stream and its changes; at each hk_render_gbuffer entry (by call
+    // parity) those counts; the latest k_gbuffer ran on gb_stream (gb_on_gs) after the caller stream at
+    // the previous call's entry (gb_wait_*: the counts there) and after frame tail gb_tail_seq; the
+    // previous hk_render_frame ran its indirect chain on the side stream only (rf_side_only)
+    uint64_t other_picks = 0, frame_st_epoch = 0;
+    hipStream_t frame_st = nullptr;
+    uint64_t entry_other[2] = {0, 0}, entry_epoch[2] = {0, 0};
+    bool gb_on_gs = false, gb_wait_valid = false, rf_side_only = false;
+    uint64_t gb_wait_other = 0, gb_wait_epoch = 0, gb_tail_seq = 0;
     // Frame-tail pipelining: the demodulation, a-trous levels and tone-sum of frame f run on
     // dn_stream next to frame f+1's light passes; render / variance are double-buffered for it.
     // Slot events: the latest tail work that read render slot r / G-buffer slot g.
@@ -109,6 +119,8 @@ struct hk_ctx {
     hipEvent_t ev_gslot[2] = {nullptr, nullptr};
     hipEvent_t ev_dn_last = nullptr;            // dn_stream, after its latest work
     bool rslot_rec[2] = {false, false}, gslot_rec[2] = {false, false};
+    // tail_end calls so far, and the one that last recorded each slot event (0: none)
+    uint64_t tail_seq = 0, rslot_seq[2] = {0, 0}, gslot_seq[2] = {0, 0};
     uint32_t rslot = 0, gslot = 0;              // current render / G-buffer slot
     bool dn_pending = false;                    // work was queued on dn_stream
     bool rf_swapped = false;                    // the latest hk_render_frame wrote the other render slot
@@ -187,7 +199,24 @@ int fail(hk_ctx* c, int code, const std::string& msg)
             return fail((c), HK_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
     } while (0)
 
-hipStream_t pick(hk_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+// Every API call that enqueues work resolves its stream here.  The frame sequence (hk_render_gbuffer,
+// hk_render_frame, hk_denoise, hk_tone_sum) uses pick_frame; the count of the other calls and a change
+// of the frame sequence's stream tell hk_render_frame what ran since k_gbuffer's wait point (the fork
+// shortcut there).
+hipStream_t pick(hk_ctx* c, void* stream)
+{
+    c->other_picks++;
+    return stream ? (hipStream_t)stream : c->stream;
+}
+hipStream_t pick_frame(hk_ctx* c, void* stream)
+{
+    const hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (s != c->frame_st) {
+        c->frame_st = s;
+        c->frame_st_epoch++;
+    }
+    return s;
+}
 
 
 #define HK_TRY(expr)            \
@@ -223,6 +252,8 @@ int tail_end(hk_ctx* c)
         hipEventRecord(c->ev_dn_last, c->dn_stream) != hipSuccess)
         return fail(c, HK_ERR_HIP, "hipEventRecord(frame tail) failed");
     c->rslot_rec[c->rslot] = c->gslot_rec[c->gslot] = true;
+    c->tail_seq++;
+    c->rslot_seq[c->rslot] = c->gslot_seq[c->gslot] = c->tail_seq;
     c->dn_pending = true;
     return HK_OK;
 }
@@ -300,9 +331,11 @@ void free_targets(hk_ctx* c)
     release(c->albedo_prev);
     c->gb_serial = true;
     c->gb_calls = 0;
+    c->gb_on_gs = c->gb_wait_valid = c->rf_side_only = false;
     c->gb_call_rec = false;
     c->rf_swapped = c->tail_open = false;
     c->rslot_rec[0] = c->rslot_rec[1] = c->gslot_rec[0] = c->gslot_rec[1] = false;
+    c->rslot_seq[0] = c->rslot_seq[1] = c->gslot_seq[0] = c->gslot_seq[1] = 0;
     c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
     release(c->accum);
     release(c->accum_out);
@@ -1112,7 +1145,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         return fail(c, HK_ERR_INVALID, "scene BVH too deep for the G-buffer traversal stack (TLAS + BLAS depth > 64)");
     if (in->jitter > HK_JITTER_TAA_SMAA) return fail(c, HK_ERR_INVALID, "unknown jitter mode");
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
+    hipStream_t st = pick_frame(c, stream);
     // Pipelining: this frame's planes go to the slot frame f-2 used.  Its readers are the work
     // enqueued on the caller's stream before the previous hk_render_gbuffer call (frame f-2's
     // passes, denoise, tone-sum, readbacks) and a post-process of frame f-1 (it reads the previous
@@ -1126,15 +1159,26 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     const uint32_t e = c->gb_calls & 1u;
     hipStream_t gs = st;
     const bool pipe = pipeline && pipeline_size(c) && !c->gb_serial && c->gb_calls > 0;
+    c->entry_other[e] = c->other_picks;
+    c->entry_epoch[e] = c->frame_st_epoch;
+    c->gb_tail_seq = 0;
+    c->gb_wait_valid = false;
     if (pipe) {
         HK_HIP(c, hipEventRecord(c->ev_gb_call[e], st));
         gs = c->gb_stream;
         // the caller stream at the previous call's entry; when that call was serial (its k_gbuffer ran
         // on st, no record), the caller stream now.  The previous pipelined k_gbuffer is earlier on gs.
-        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[c->gb_call_rec ? e ^ 1u : e], 0));
+        const uint32_t w = c->gb_call_rec ? e ^ 1u : e;
+        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[w], 0));
+        c->gb_wait_valid = true;
+        c->gb_wait_other = c->entry_other[w];
+        c->gb_wait_epoch = c->entry_epoch[w];
         if (c->post_pending) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_post, 0));
         // frame f-2's denoise on dn_stream read that slot
-        if (c->gslot_rec[c->gslot ^ 1u]) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gslot[c->gslot ^ 1u], 0));
+        if (c->gslot_rec[c->gslot ^ 1u]) {
+            HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gslot[c->gslot ^ 1u], 0));
+            c->gb_tail_seq = c->gslot_seq[c->gslot ^ 1u];
+        }
     } else {
         HK_TRY(gb_join(c, st));
     }
@@ -1203,6 +1247,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         c->gb_pending = true;
     }
     c->gb_call_rec = pipe;
+    c->gb_on_gs = gs != st;
     c->gb_serial = false;
     c->gb_calls++;
     c->albedo_fresh = true;
@@ -1296,21 +1341,31 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     float want = settings->upscale_ratio < 1.0f ? 1.0f : (settings->upscale_ratio > 2.0f ? 2.0f : settings->upscale_ratio);
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
+    hipStream_t st = pick_frame(c, stream);
     // Frame-tail pipelining: with all three channels rendered, this frame's render / variance
     // targets are the other slot, last read by frame f-2's denoise / tone-sum, so frame f-1's tail
     // (on dn_stream) can still be running while this frame's light passes start.
     const bool swap = dn_pipeline_enabled(c) && settings->indirect_bounces >= 1u;
-    // (k_albedo rewrites the albedo plane a previous tail may still read: full join then)
-    HK_TRY(gb_join(c, st, !swap || !c->albedo_fresh));
+    // This frame's G-buffer ran pipelined on gb_stream after the caller stream at the previous
+    // hk_render_gbuffer's entry (W), and since W only the frame sequence ran, on this stream (no other
+    // API call, no stream change): frame f-1's hk_render_frame, denoise, tone-sum and this frame's
+    // hk_render_gbuffer.  See the fork below.
+    const bool gb_fresh = c->gb_on_gs && c->gb_wait_valid && c->other_picks == c->gb_wait_other &&
+                          c->frame_st_epoch == c->gb_wait_epoch && c->gb_pending;
     if (swap) {
         for (int ch = 0; ch < 3; ++ch) {
             std::swap(c->render[ch], c->render_alt[ch]);
             std::swap(c->variance[ch], c->variance_alt[ch]);
         }
         c->rslot ^= 1u;
-        if (c->rslot_rec[c->rslot]) HK_HIP(c, hipStreamWaitEvent(st, c->ev_rslot[c->rslot], 0));
     }
+    // the render slot's last reader (frame f-2's tail) — also covered by ev_gb_done when k_gbuffer waited
+    // for that tail or a later one (dn_stream is in order); each wait packet costs the stream latency
+    const bool slot_wait = swap && c->rslot_rec[c->rslot];
+    const bool slot_covered = gb_fresh && c->gb_pending && c->rslot_seq[c->rslot] <= c->gb_tail_seq;
+    if (slot_wait && !slot_covered) HK_HIP(c, hipStreamWaitEvent(st, c->ev_rslot[c->rslot], 0));
+    // (k_albedo rewrites the albedo plane a previous tail may still read: full join then)
+    HK_TRY(gb_join(c, st, !swap || !c->albedo_fresh));
     c->rf_swapped = swap;
     c->tail_open = false;
     if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
@@ -1370,19 +1425,34 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // direct_lit + emissive (fused per pixel) and the one-bounce indirect pass in ONE launch
     // (k_light_merged), replacing the indirect side stream and its fork / join events.  It needs the
     // fused launch's conditions (identity reprojection) and a direct pass that does not stage the scene.
-    // By default only on small frames without spatial reuse: there each kernel lasts about one wave
-    // lifetime and the events' latency is a fifth of the frame (cornell 8-way stripe 0.144 -> 0.121
-    // ms/frame); on larger frames the two streams overlap better (4-way stripe 0.173 vs 0.177, 1080p
-    // 0.474 vs 0.511, city 4K 6.25 vs 7.21: spatial reuse would wait for the direct pass).  Not in the
-    // isolated-kernel measurement mode (HK_CHANNEL_STREAMS=0).  HK_MERGE=1: whenever possible, 0: never.
+    // By default on the frames that are not pipelined (pipeline_size: < 1.2 Mpx, the 2- to 8-way
+    // stripes of 1080p) and have no spatial reuse: there each kernel lasts a few wave lifetimes and
+    // the fork / join events' latency is a large part of the frame (cornell stripes 2-way 0.270 ->
+    // 0.263, 4-way 0.164 -> 0.160, 8-way 0.144 -> 0.112 ms/frame with the serial path's event
+    // elision); on pipelined frames the streams overlap better (1080p 0.472 vs 0.486, city 4K 6.25
+    // vs 7.21: spatial reuse would wait for the direct pass).  Not in the isolated-kernel measurement
+    // mode (HK_CHANNEL_STREAMS=0).  HK_MERGE=1: whenever possible, 0: never.
     const char* me = getenv("HK_MERGE");
     const bool merge_possible = identity && fork && !multi && !wf && !light_lds_direct(A) && !getenv("HK_NO_FUSE");
-    const bool merge_default = (double)c->s[0] * (double)c->s_rows <= 4.0e5 && !settings->indirect_spatial_reuse &&
-                               !settings->emissive_spatial_reuse;
+    const bool merge_default = !pipeline_size(c) && !settings->indirect_spatial_reuse && !settings->emissive_spatial_reuse;
     const bool merge = merge_possible && (me ? me[0] == '1' : merge_default);
     if (fork && !merge) {
-        HK_HIP(c, hipEventRecord(c->ev_fork, st));
-        HK_HIP(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
+        if (gb_fresh && c->rf_side_only && swap && c->albedo_fresh) {
+            // The fork marker would make the side stream wait for the caller stream here.  What the
+            // indirect chain reads of that stream's work: the work before W (k_gbuffer waited for it),
+            // frame f-1's hk_render_frame (its indirect chain ran on the side stream itself; the rest of
+            // it — k_albedo did not run, direct / emissive passes, their masks — writes buffers the chain
+            // does not read), frame f-1's tail (on dn_stream; it reads the other render slot and no
+            // reservoir), frame f-2's tail (the render slot this frame writes: covered when k_gbuffer
+            // waited for that tail or a later one) and the G-buffer.  So the side stream waits for
+            // ev_gb_done alone: every packet queued ahead of a kernel delays it, and the side stream
+            // shares its hardware queue with gb_stream (cornell 1080p 0.472 -> 0.45 ms/frame).
+            if (slot_wait && !slot_covered) HK_HIP(c, hipStreamWaitEvent(s2, c->ev_rslot[c->rslot], 0));
+            HK_HIP(c, hipStreamWaitEvent(s2, c->ev_gb_done, 0));
+        } else {
+            HK_HIP(c, hipEventRecord(c->ev_fork, st));
+            HK_HIP(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
+        }
         fork_events = true;
     }
     HK_TRY(bg_mask(c, 0, A, identity, !settings->emissive_spatial_reuse, st, C0));
@@ -1421,6 +1491,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         HK_HIP(c, hipEventRecord(c->ev_join[1], s2));
         HK_HIP(c, hipStreamWaitEvent(st, c->ev_join[1], 0));
     }
+    c->rf_side_only = fork_events && c->albedo_fresh;  // (no k_albedo on the caller stream)
     if (swap) HK_HIP(c, hipEventRecord(c->ev_rf, st));
     HK_HIP(c, hipGetLastError());
     return HK_OK;
@@ -1434,7 +1505,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     if (!settings->denoise) return HK_OK;
     if (c->stripe_n >= 2) return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude the denoiser: it reads neighbours");
     (void)hipSetDevice(c->device);
-    hipStream_t caller = pick(c, stream);
+    hipStream_t caller = pick_frame(c, stream);
     // after a slot-swapping hk_render_frame: on dn_stream, next to the following frame's passes
     const bool async = c->rf_swapped;
     hipStream_t st = async ? c->dn_stream : caller;
@@ -1476,7 +1547,7 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     (void)hipSetDevice(c->device);
     // after a slot-swapping hk_render_frame: on dn_stream (after that frame's denoise, if any)
     const bool async = c->rf_swapped;
-    hipStream_t st = async ? c->dn_stream : pick(c, stream);
+    hipStream_t st = async ? c->dn_stream : pick_frame(c, stream);
     if (async) HK_TRY(tail_begin(c));
     else HK_TRY(gb_join(c, st));
     hk_frame_inputs dummy;
