@@ -108,6 +108,13 @@ struct hk_ctx {
     uint64_t entry_other[2] = {0, 0}, entry_epoch[2] = {0, 0};
     bool gb_on_gs = false, gb_wait_valid = false, rf_side_only = false;
     uint64_t gb_wait_other = 0, gb_wait_epoch = 0, gb_tail_seq = 0;
+    // hk_render_frame calls (rf_seq) and the latest one that recorded ev_rf (rf_rec_seq, with the counts
+    // there); the ev_rf the open tail waited for (tail_rf), per G-buffer slot the one its last tail
+    // waited for; per call parity, at hk_render_gbuffer's entry: the latest hk_render_frame and whether
+    // only the frame sequence ran since it recorded ev_rf (entry_clean)
+    uint64_t rf_seq = 0, rf_rec_seq = 0, rf_other = 0, rf_epoch = 0, tail_rf = 0;
+    uint64_t gslot_rf[2] = {0, 0}, entry_rf[2] = {0, 0};
+    bool entry_clean[2] = {false, false};
     // Frame-tail pipelining: the demodulation, a-trous levels and tone-sum of frame f run on
     // dn_stream next to frame f+1's light passes; render / variance are double-buffered for it.
     // Slot events: the latest tail work that read render slot r / G-buffer slot g.
@@ -240,8 +247,11 @@ int gb_join(hk_ctx* c, hipStream_t st, bool with_denoise = true)
 // the render / G-buffer slots it read
 int tail_begin(hk_ctx* c)
 {
-    if (!c->tail_open && hipStreamWaitEvent(c->dn_stream, c->ev_rf, 0) != hipSuccess)
-        return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(frame) failed");
+    if (!c->tail_open) {
+        if (hipStreamWaitEvent(c->dn_stream, c->ev_rf, 0) != hipSuccess)
+            return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(frame) failed");
+        c->tail_rf = c->rf_rec_seq;
+    }
     c->tail_open = true;
     return HK_OK;
 }
@@ -254,6 +264,7 @@ int tail_end(hk_ctx* c)
     c->rslot_rec[c->rslot] = c->gslot_rec[c->gslot] = true;
     c->tail_seq++;
     c->rslot_seq[c->rslot] = c->gslot_seq[c->gslot] = c->tail_seq;
+    c->gslot_rf[c->gslot] = c->tail_rf;
     c->dn_pending = true;
     return HK_OK;
 }
@@ -336,6 +347,8 @@ void free_targets(hk_ctx* c)
     c->rf_swapped = c->tail_open = false;
     c->rslot_rec[0] = c->rslot_rec[1] = c->gslot_rec[0] = c->gslot_rec[1] = false;
     c->rslot_seq[0] = c->rslot_seq[1] = c->gslot_seq[0] = c->gslot_seq[1] = 0;
+    c->gslot_rf[0] = c->gslot_rf[1] = 0;
+    c->entry_clean[0] = c->entry_clean[1] = false;
     c->upscale_wh[0] = c->upscale_wh[1] = c->taa_wh[0] = c->taa_wh[1] = 0;
     release(c->accum);
     release(c->accum_out);
@@ -1161,6 +1174,9 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     const bool pipe = pipeline && pipeline_size(c) && !c->gb_serial && c->gb_calls > 0;
     c->entry_other[e] = c->other_picks;
     c->entry_epoch[e] = c->frame_st_epoch;
+    c->entry_rf[e] = c->rf_seq;
+    c->entry_clean[e] = c->rf_seq > 0 && c->rf_rec_seq == c->rf_seq && c->other_picks == c->rf_other &&
+                        c->frame_st_epoch == c->rf_epoch;
     c->gb_tail_seq = 0;
     c->gb_wait_valid = false;
     if (pipe) {
@@ -1169,15 +1185,22 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         // the caller stream at the previous call's entry; when that call was serial (its k_gbuffer ran
         // on st, no record), the caller stream now.  The previous pipelined k_gbuffer is earlier on gs.
         const uint32_t w = c->gb_call_rec ? e ^ 1u : e;
-        HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[w], 0));
+        // Frame f-2's tail (dn_stream) read this slot; it waited for ev_rf of a hk_render_frame (gslot_rf).
+        // When that is the one whose ev_rf marked the caller stream where the previous call's entry
+        // marker stands (nothing but the frame sequence ran in between: entry_clean) or a later one, the
+        // tail's event implies the entry marker, and k_gbuffer waits for the tail alone: one packet fewer
+        // ahead of it in the queue it shares with the indirect chain.
+        const uint32_t g = c->gslot ^ 1u;
+        const bool tail_covers = c->gb_call_rec && c->gslot_rec[g] && c->entry_clean[w] && c->entry_rf[w] > 0 &&
+                                 c->gslot_rf[g] >= c->entry_rf[w];
+        if (!tail_covers) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gb_call[w], 0));
         c->gb_wait_valid = true;
         c->gb_wait_other = c->entry_other[w];
         c->gb_wait_epoch = c->entry_epoch[w];
         if (c->post_pending) HK_HIP(c, hipStreamWaitEvent(gs, c->ev_post, 0));
-        // frame f-2's denoise on dn_stream read that slot
-        if (c->gslot_rec[c->gslot ^ 1u]) {
-            HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gslot[c->gslot ^ 1u], 0));
-            c->gb_tail_seq = c->gslot_seq[c->gslot ^ 1u];
+        if (c->gslot_rec[g]) {
+            HK_HIP(c, hipStreamWaitEvent(gs, c->ev_gslot[g], 0));
+            c->gb_tail_seq = c->gslot_seq[g];
         }
     } else {
         HK_TRY(gb_join(c, st));
@@ -1492,7 +1515,13 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         HK_HIP(c, hipStreamWaitEvent(st, c->ev_join[1], 0));
     }
     c->rf_side_only = fork_events && c->albedo_fresh;  // (no k_albedo on the caller stream)
-    if (swap) HK_HIP(c, hipEventRecord(c->ev_rf, st));
+    c->rf_seq++;
+    if (swap) {
+        HK_HIP(c, hipEventRecord(c->ev_rf, st));
+        c->rf_rec_seq = c->rf_seq;
+        c->rf_other = c->other_picks;
+        c->rf_epoch = c->frame_st_epoch;
+    }
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
