@@ -936,22 +936,26 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
 // box equals the child box (k_build_wide): its box test is then the descent's / pop's comparison.
 // Leaf boxes are the triangle's / instance's box, as the reference walk tests them.
 constexpr int GB_STACK = 64;
-// Stack entries (node, entry distance): the first GB_STACK_LDS live in the workgroup's LDS
-// (entry-major, one uint2 per thread per level: conflict-free), deeper ones in private scratch.
+// Stack entries (node, entry distance) live in the workgroup's LDS (entry-major, one uint2 per thread
+// per level: conflict-free): all of them when the scene's stack bound is <= GB_STACK_LDS (SHALLOW,
+// exactly that many levels), otherwise the first GB_DEEP_LDS, deeper ones in private scratch.
 constexpr int GB_STACK_LDS = 16;
+// a deeper scene's stack: its first GB_DEEP_LDS levels in LDS, the rest in private scratch
+constexpr int GB_DEEP_LDS = 8;
 // SHALLOW: the scene's stack bound fits the LDS levels (hk_runtime gb_stack_need), so there is no
 // private overflow array (no scratch allocation for the kernel's waves)
-template <bool SHALLOW>
+// LVL: the LDS levels of a deep scene's stack (the rest in scratch)
+template <bool SHALLOW, int LVL = GB_STACK_LDS>
 struct GbStackT {
-    uint2* lds;  // [GB_STACK_LDS][blockDim.x], or null
-    uint32_t node[SHALLOW ? 1 : GB_STACK - GB_STACK_LDS];
-    float t[SHALLOW ? 1 : GB_STACK - GB_STACK_LDS];
+    uint2* lds;  // [LVL][blockDim.x], or null
+    uint32_t node[SHALLOW ? 1 : GB_STACK - LVL];
+    float t[SHALLOW ? 1 : GB_STACK - LVL];
     int sp;
     HKD void push(uint32_t n, float tt)
     {
-        if (SHALLOW || (lds && sp < GB_STACK_LDS)) lds[sp * 256 + threadIdx.x] = make_uint2(n, __float_as_uint(tt));
+        if (SHALLOW || (lds && sp < LVL)) lds[sp * 256 + threadIdx.x] = make_uint2(n, __float_as_uint(tt));
         else {
-            const int k = lds ? sp - GB_STACK_LDS : sp;
+            const int k = lds ? sp - LVL : sp;
             node[k] = n;
             t[k] = tt;
         }
@@ -959,12 +963,12 @@ struct GbStackT {
     }
     HKD void top(uint32_t& n, float& tt) const
     {
-        if (SHALLOW || (lds && sp < GB_STACK_LDS)) {
+        if (SHALLOW || (lds && sp < LVL)) {
             const uint2 e = lds[sp * 256 + threadIdx.x];
             n = e.x;
             tt = __uint_as_float(e.y);
         } else {
-            const int k = lds ? sp - GB_STACK_LDS : sp;
+            const int k = lds ? sp - LVL : sp;
             n = node[k];
             tt = t[k];
         }
@@ -1012,7 +1016,7 @@ HKD bool gb_descend(GbStack& s, const Ray& ray, float4 a, float4 b, float4 c, fl
 // The same walk with the TLAS and BLAS steps in one loop (as traverse_top): each iteration
 // visits one wide entry of the lane's current level, so a wave's lanes do not wait for each
 // other's BLAS walks.  Identical visits, pushes, pops and hit updates per lane.
-template <bool SHALLOW = false>
+template <bool SHALLOW = false, int LVL = GB_STACK_LDS>
 HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = nullptr)
 {
     Hit hit;
@@ -1021,7 +1025,7 @@ HKD Hit closest_hit_ordered(const Scene& sc, const Ray& ray, uint2* lds_stack = 
     hit.instance_index = HK_U32_MAX;
     hit.primitive_index = HK_U32_MAX;
     if (sc.n_instance_nodes == 0u) return hit;
-    GbStackT<SHALLOW> s;
+    GbStackT<SHALLOW, LVL> s;
     s.sp = 0;
     s.lds = lds_stack;
     uint32_t p = 0u;          // subtree start of the current level (mesh-local in a BLAS)
