@@ -742,34 +742,6 @@ HKD bool traverse_bottom(const Scene& sc, Hit& hit, const Ray& ray, uint32_t nod
         index = next;
     }
     return intersected;
-    while (index < node_count) {
-        f3 mn, mx;
-        uint32_t entry, exit;
-        load_node(sc.asset_nodes, node_offset + index, mn, entry, mx, exit);
-        // leaves carry their triangle's box (k_fill_blas_leaves): the same slab test as
-        // light.wgsl:411-413 on the recomputed box, before the triangle is fetched
-        const bool pass = intersects_aabb(ray, mn, mx) < hit.distance;
-        if (entry >= HK_BVH_LEAF_FLAG) {
-            if (pass) {
-                uint32_t primitive_index = prim_offset + entry - HK_BVH_LEAF_FLAG;
-                f3 a, b, c;
-                load_triangle(sc.primitives, primitive_index, a, b, c);
-                f2 uv;
-                float d = intersects_triangle(ray, a, b, c, uv);
-                if (d < hit.distance) {
-                    hit.distance = d;
-                    hit.uv = uv;
-                    hit.primitive_index = primitive_index;
-                    intersected = true;
-                    if (d < early_distance) return intersected;
-                }
-            }
-            index = exit;
-        } else {
-            index = pass ? entry : exit;
-        }
-    }
-    return intersected;
 }
 
 HKD f3 world_to_local_point(const hk_instance& in, f3 p)
