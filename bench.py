@@ -219,6 +219,16 @@ def load_lane_efficiency(config: str, wavefront: bool):
         return None
 
 
+def json_stdout():
+    """The bench's stdout carries its one JSON line only: file descriptor 1 is pointed at stderr for the
+    rest of the run (RCCL prints its version banner on descriptor 1 when the communicator is created), and the
+    JSON line goes to the original stdout through the returned file."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +237,7 @@ def main():
     ap.add_argument("--config", default="cornell-1080p-nee", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
     args = ap.parse_args()
+    out = json_stdout()
 
     cfg = CONFIGS[args.config]
     rank = int(os.environ.get("RANK", 0))
@@ -238,9 +249,12 @@ def main():
     # collectives through host memory) — a correctness check of the band / gather / reduction
     # logic, never a measurement.  The real N-GPU run uses RCCL over xGMI.
     rehearsal = os.environ.get("HK_BENCH_REHEARSAL") == "1"
+    # HK_BENCH_DIST=1: the collective path at world size 1 too (RCCL init, the per-frame all-gather and the
+    # reductions on one GPU) — a check of the RCCL calls on the hardware; its line is not the N=1 result
+    dist_on = world > 1 or os.environ.get("HK_BENCH_DIST") == "1"
     device = 0 if rehearsal else local
     torch.cuda.set_device(device)
-    if world > 1:
+    if dist_on:
         if rehearsal:
             dist.init_process_group("gloo")
         else:
@@ -255,7 +269,7 @@ def main():
     s = st.to_c()
 
     # rows of this rank (hikari_amd/bands.py): interleaved stripes, or a contiguous band + halo
-    stripes = world > 1 and use_stripes(cfg["spatial"], cfg["denoise"])
+    stripes = dist_on and use_stripes(cfg["spatial"], cfg["denoise"])
     r = HikariRenderer(device)
     r.set_noise()
     r.upload_scene(scene)
@@ -267,7 +281,7 @@ def main():
     if stripes:
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
-    elif world > 1:
+    elif dist_on:
         b = band_of(rank, world, H)
         band = b.rows
         r.resize(W, H, 1.0, b.y0, b.rows)
@@ -282,7 +296,7 @@ def main():
     # while frame f+1 renders; a buffer is reused only after its previous gather completed
     band_t = [torch.zeros((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
     full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
-        if world > 1 else None
+        if dist_on else None
     pending = [None, None]
     if stripes:  # stripes back in frame order, on a side stream after each gather
         frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
@@ -330,7 +344,7 @@ def main():
                 r.accumulate(k == 0, sp)
         if spp > 1:
             r.resolve_accumulation(sp)
-        if world > 1:
+        if dist_on:
             k = f & 1
             if pending[k] is not None:
                 pending[k].wait()  # device-side: the stream waits for that gather
@@ -362,7 +376,7 @@ def main():
 
     for f in range(args.warmup):
         step(f)
-    if world > 1:
+    if dist_on:
         drain()
         dist.barrier()
     torch.cuda.synchronize()
@@ -372,13 +386,13 @@ def main():
     r.set_kernel_timing_interval(max(1, min(args.steps, int(os.environ.get("HK_BENCH_TIMING_EVERY", "4")))))
     r.enable_kernel_timing(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for f in range(args.warmup, args.warmup + args.steps):
         step(f)
-    if world > 1:
+    if dist_on:
         drain()  # every timed frame's gather is complete inside the timed region
         dist.barrier()
     torch.cuda.synchronize()
@@ -391,7 +405,7 @@ def main():
     c = r.counters()
     rays = c["traverse_top"] + c["traverse_emitter"]
     primary = c["primary"]
-    if world > 1:
+    if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -520,9 +534,9 @@ def main():
             result["cpu_baseline"] = cpu_baseline(desc, camera_at, lights, st, W, H, args.cpu_budget)
         else:
             result["cpu_baseline"] = None
-        print(json.dumps(result))
+        print(json.dumps(result), file=out, flush=True)
     r.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
