@@ -212,7 +212,14 @@ struct Counters {
     unsigned long long* top;
     unsigned long long* emitter;
     unsigned long long* primary;
+    // persistent-wave tile claims (k_indirect_persist): PERSIST_KINDS blocks of PERSIST_LINES 128-B lines,
+    // zero between launches
+    unsigned long long* persist;
 };
+constexpr uint32_t PERSIST_SHARDS = 8;               // claim counters per block (one per XCD of the round-robin)
+constexpr uint32_t PERSIST_LINE = 16;                // u64 per 128-B line
+constexpr uint32_t PERSIST_LINES = PERSIST_SHARDS + 1;  // + the exit counter
+constexpr uint32_t PERSIST_KINDS = 4;
 
 template <int PLAN>
 HKD Scene stage_scene(const Scene& g, uint32_t* lds)

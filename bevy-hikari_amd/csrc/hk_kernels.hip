@@ -935,6 +935,65 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
     wave_count(A.cnt.emitter, n_emitter);
 }
 
+// ------------------------------------------------------------------ persistent waves (the north star's layout)
+// HK_PERSIST=1: a light pass as persistent waves instead of one workgroup per 16x16 tile.  The grid is what
+// the GPU holds resident (occupancy x CUs); each wave claims 8x8-pixel tiles one at a time from a claim
+// counter (workgroup b uses counter b % 8 — the XCD the round-robin dispatch puts it on — and counter k hands
+// out tiles k, k + 8, k + 16, ... in raster order), runs the unchanged per-pixel body on the tile's 64 pixels
+// and exits once its counter is exhausted.  Every wave makes exactly one failing claim, so every wave
+// reaches the exit; the last wave out (an exit counter) zeroes the block for the next launch.  Workgroups
+// stage the scene into LDS once instead of once per tile, and waves whose tiles are cheap (background) take
+// more of them.  The per-pixel code is the tile kernel's, so every stored word is unchanged.
+enum PersistKind : uint32_t { PERSIST_INDIRECT = 0, PERSIST_DIRECT = 1 };
+template <class Body>
+HKD void persist_tiles(const FrameArgs& A, uint32_t kind, Body body)
+{
+    const Frame& F = A.F;
+    const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0;
+    const int32_t w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : F.s_rows;
+    const uint32_t tiles_x = (F.s[0] + 7u) >> 3;
+    const uint32_t n = tiles_x * ((uint32_t)(w1 - w0 + 7) >> 3);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t shards = gridDim.x < PERSIST_SHARDS ? gridDim.x : PERSIST_SHARDS, shard = blockIdx.x % shards;
+    unsigned long long* block = A.cnt.persist + (size_t)kind * PERSIST_LINES * PERSIST_LINE;
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = (uint32_t)atomicAdd(block + shard * PERSIST_LINE, 1ull);
+        k = __shfl(k, 0, 64);
+        const uint32_t t = shard + shards * k;
+        if (t >= n) break;
+        const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+        const int32_t x = (int32_t)(tx * 8u + (lane & 7u));
+        const int32_t ly = w0 + (int32_t)(ty * 8u + (lane >> 3));
+        body(x, global_row(F, ly, F.s_row0), (uint32_t)x < F.s[0] && ly < w1);
+    }
+    if (lane == 0) {
+        __threadfence();
+        unsigned int* exited = reinterpret_cast<unsigned int*>(block + PERSIST_SHARDS * PERSIST_LINE);
+        if (atomicAdd(exited, 1u) == gridDim.x * 4u - 1u) {  // every other wave has made its last claim
+            for (uint32_t k = 0; k < PERSIST_SHARDS; ++k) atomicExch(block + k * PERSIST_LINE, 0ull);
+            atomicExch(exited, 0u);
+        }
+    }
+}
+template <bool MULTI, bool LDS>
+__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect_persist(FrameArgs A, ChannelArgs C)
+{
+    Scene sc = A.sc;
+    if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+    uint32_t n_top = 0, n_emitter = 0;
+    persist_tiles(A, PERSIST_INDIRECT, [&](int32_t x, int32_t y, bool active) {
+        uint32_t t = 0, e = 0;
+        if (active) indirect_body<MULTI>(A, sc, C, x, y, t, e);
+        if (y >= A.F.count_y0 && y < A.F.count_y1) {
+            n_top += t;
+            n_emitter += e;
+        }
+    });
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
 // The fused direct/emissive pass and the one-bounce indirect pass in ONE launch.  They read the same
 // G-buffer and write disjoint buffers (reservoirs 0-5 and the direct / emissive planes, reservoirs 6-9
 // and the indirect planes: light.rs:518-546), so their workgroups are independent and are interleaved
@@ -1760,10 +1819,60 @@ void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const Channe
     if (lds) launch_fused_v<true>(A, C0, C1, vd, ve, g, lds, st);
     else launch_fused_v<false>(A, C0, C1, vd, ve, g, 0, st);
 }
+// workgroups of a persistent launch: what the device holds resident of this kernel, at most one 8x8 tile per wave
+static uint32_t persist_grid(const void* kernel, uint32_t lds, const Frame& F)
+{
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    }
+    // resident workgroups per CU, per (kernel, LDS bytes): queried once
+    struct Occ {
+        const void* kernel;
+        uint32_t lds;
+        int per_cu;
+    };
+    static Occ cache[16];
+    static int cached = 0;
+    int per_cu = -1;
+    for (int i = 0; i < cached; ++i)
+        if (cache[i].kernel == kernel && cache[i].lds == lds) per_cu = cache[i].per_cu;
+    if (per_cu < 0) {
+        per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds);
+        if (cached < 16) cache[cached++] = Occ{kernel, lds, per_cu};
+    }
+    const int32_t rows = F.win_rows > 0 ? F.win_rows : F.s_rows;
+    const uint32_t tiles8 = ((F.s[0] + 7u) / 8u) * (((uint32_t)rows + 7u) / 8u);
+    const uint32_t g = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
+    const uint32_t need = (tiles8 + 3u) / 4u;
+    return need < g ? (need > 0u ? need : 1u) : g;
+}
+static bool persist_mode()
+{
+    const char* e = getenv("HK_PERSIST");  // read per launch (tests switch it in-process)
+    return e && e[0] == '1';
+}
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st)
 {
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, true);
+    if (persist_mode()) {
+#define HK_PERSIST_LAUNCH(M_, L_)                                                                                    \
+    hipLaunchKernelGGL((k_indirect_persist<M_, L_>), dim3(persist_grid((const void*)k_indirect_persist<M_, L_>, lds, A.F)), \
+                       dim3(256), lds, st, A, C)
+        if (multi) {
+            if (lds) HK_PERSIST_LAUNCH(true, true);
+            else HK_PERSIST_LAUNCH(true, false);
+        } else {
+            if (lds) HK_PERSIST_LAUNCH(false, true);
+            else HK_PERSIST_LAUNCH(false, false);
+        }
+#undef HK_PERSIST_LAUNCH
+        return;
+    }
     if (multi) {
         if (lds) hipLaunchKernelGGL((k_indirect<true, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_indirect<true, false>), g, dim3(256), 0, st, A, C);

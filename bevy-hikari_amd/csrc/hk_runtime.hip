@@ -23,10 +23,11 @@
 using namespace hk;
 
 namespace {
-constexpr int32_t BAND_HALO = 40;
+constexpr int32_t BAND_HALO = 40;  // >= 36 rows: 20 (spatial reuse) + 15 (a-trous) + 1 (variance blur)
 // 3 counters (top, emitter, primary) x COUNTER_SHARDS lines of 64 B
 constexpr size_t COUNTER_SPAN = (size_t)COUNTER_SHARDS * COUNTER_STRIDE;  // u64 per counter
-constexpr size_t COUNTER_BYTES = 3 * COUNTER_SPAN * sizeof(unsigned long long);  // >= 36 rows: 20 (spatial reuse) + 15 (a-trous) + 1 (variance blur)
+constexpr size_t COUNTER_BYTES = 3 * COUNTER_SPAN * sizeof(unsigned long long);
+constexpr size_t PERSIST_BYTES = (size_t)PERSIST_KINDS * PERSIST_LINES * PERSIST_LINE * sizeof(unsigned long long);
 
 struct TimedLaunch {
     const char* name;
@@ -167,6 +168,7 @@ struct hk_ctx {
     uint32_t accum_n = 0;
     // counters (top, emitter, primary)
     unsigned long long* counters = nullptr;
+    unsigned long long* persist = nullptr;  // persistent-wave tile claim counters (Counters::persist)
     // wavefront indirect pass (hk_set_wavefront): queues, SoA hit records, control words
     bool wavefront = false;
     uint32_t* wf_queue1 = nullptr;
@@ -557,6 +559,7 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.cnt.top = c->counters;
     A.cnt.emitter = c->counters + COUNTER_SPAN;
     A.cnt.primary = c->counters + 2 * COUNTER_SPAN;
+    A.cnt.persist = c->persist;
     return A;
 }
 
@@ -654,7 +657,8 @@ int hk_create(int device, hk_ctx** out)
     hk_ctx* c = new hk_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counters, COUNTER_BYTES) != hipSuccess || hipMemset(c->counters, 0, COUNTER_BYTES) != hipSuccess) {
+        hipMalloc(&c->counters, COUNTER_BYTES) != hipSuccess || hipMemset(c->counters, 0, COUNTER_BYTES) != hipSuccess ||
+        hipMalloc(&c->persist, PERSIST_BYTES) != hipSuccess || hipMemset(c->persist, 0, PERSIST_BYTES) != hipSuccess) {
         delete c;
         return HK_ERR_HIP;
     }
@@ -718,6 +722,7 @@ void hk_destroy(hk_ctx* c)
     release(c->tex_lut);
     release(c->noise);
     release(c->counters);
+    release(c->persist);
     for (auto& t : c->pending) {
         c->event_pool.push_back(t.start);
         c->event_pool.push_back(t.stop);
