@@ -292,14 +292,15 @@ def test_forced_kernel_variants_bit_exact(monkeypatch, lds):
     frame: k_direct_lit_w4 (4 waves per SIMD; HK_DIRECT_W4_MIN_PX=0 with HK_NO_FUSE), the fused
     direct+emissive launch next to the indirect side stream (HK_FUSE_MIN_PX=0, HK_MERGE=0) and the
     merged direct+indirect launch (k_light_merged, HK_MERGE=1: the default only for small frames without
-    spatial reuse; here with spatial reuse after it), each with and without LDS scene staging."""
+    spatial reuse; here with spatial reuse after it) and the persistent-wave indirect pass
+    (k_indirect_persist, HK_PERSIST=1, an opt-in), each with and without LDS scene staging."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     monkeypatch.setenv("HK_LDS_SCENE", lds)
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
     s = st.to_c()
     for env in ({"HK_DIRECT_W4_MIN_PX": "0", "HK_NO_FUSE": "1"}, {"HK_FUSE_MIN_PX": "0", "HK_MERGE": "0"},
-                {"HK_MERGE": "1"}):
+                {"HK_MERGE": "1"}, {"HK_PERSIST": "1", "HK_MERGE": "0"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         scene, cam, lights, r, o = _pair("cornell", w, h, st, threads=0)
