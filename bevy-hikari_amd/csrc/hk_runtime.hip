@@ -1434,9 +1434,17 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     const double fuse_min_px = fmin ? atof(fmin) : (double)(1u << 20);
     const bool fuse = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f &&
                       (double)c->s[0] * (double)c->s_rows >= fuse_min_px && !getenv("HK_NO_FUSE");
-    // background elision under the identity reprojection (every store on the thread's own pixel);
-    // the separate launches share the pair's mask (direct_pass)
+    // background elision (bg_mask, hk_kernels.hip bg_elide); the separate launches share the pair's mask
+    // (direct_pass).  A background pixel's own targets (temporal record, render, variance) are written by
+    // that pixel alone, so they elide with or without motion.  Under motion the temporal passes also scatter
+    // into the previous spatial buffer at reprojected pixels (light.wgsl:1092-1095, 1199-1202, 1453-1457),
+    // and the record they scatter there is the zero reservoir (check_previous_reservoir zeroes it before the
+    // store): the indirect channel's background constant, so its pair bit stays true; the direct pair's
+    // background record is background_reservoir (count 1), so its pair elides only under the identity
+    // reprojection — bg_elide rewrites a background byte without the pair bit whenever the frame's targets
+    // do not include it, so a motion frame clears it.
     const bool identity = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f;
+    const bool elide = c->albedo_fresh && c->ratio == 1.0f;
     ChannelArgs C2 = channel(c, A.F.number, 2);
     // spatial view planes (ChannelArgs::view): the indirect temporal pass writes them next to the records
     // it stores, this frame's spatial pass reads its neighbours from them.  Only when that temporal pass
@@ -1483,12 +1491,12 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         }
         fork_events = true;
     }
-    HK_TRY(bg_mask(c, 0, A, identity, !settings->emissive_spatial_reuse, st, C0));
+    HK_TRY(bg_mask(c, 0, A, elide, identity && !settings->emissive_spatial_reuse, st, C0));
     C1.bg = C0.bg;
     C1.bg_need = C0.bg_need;
     if (merge) {
         // (the elision mask of the indirect channel is prepared on the launch stream)
-        HK_TRY(bg_mask(c, 1, A, identity, !settings->indirect_spatial_reuse, st, C2));
+        HK_TRY(bg_mask(c, 1, A, elide, !settings->indirect_spatial_reuse, st, C2));
         timed(c, "light_merged", st, [&] { launch_light_merged(A, C0, C1, C2, st); });
         if (settings->emissive_spatial_reuse)
             timed(c, "emissive_spatial_reuse", st, [&] { launch_spatial(AS, C1, true, st); });
@@ -1503,7 +1511,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         }
         if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(AS, C1, true, s1); });
         // (the wavefront pass elides in its generation stage, which classifies every pixel)
-        HK_TRY(bg_mask(c, 1, A, identity, !settings->indirect_spatial_reuse, s2, C2));
+        HK_TRY(bg_mask(c, 1, A, elide, !settings->indirect_spatial_reuse, s2, C2));
         if (wf) {
             HK_TRY(ensure_wavefront(c));
             WfArgs W{c->wf_queue1, c->wf_keys, c->wf_queue2, c->wf_hit, c->wf_hit_t, c->wf_ctl, c->count[6] + 1u,
