@@ -77,7 +77,7 @@ BYTES_PER_PIXEL = {
 # fused direct/emissive launch and of the indirect pass reads its position texel (16) and its mask
 # byte (1) and stores nothing — its targets already hold the constant zero words — except, when the
 # channel's spatial reuse runs (it rewrites the pair with other bits), both spatial-pair records
-# (2 x 64); a G-buffer miss reads its mask byte only.  Not on with HK_NO_BG_ELIDE=1.
+# (2 x 64); a G-buffer miss reads its mask byte only.  Not with option bg_elision = 0.
 BG_ELIDED_BYTES = {"gbuffer": (None, 1, 1),  # a miss: its mask byte (the slot already holds the zero texels)
                    "direct_lit_emissive": ("emissive_spatial_reuse", 17, 145),
                    "indirect_lit_ambient": ("indirect_spatial_reuse", 17, 145),
@@ -86,11 +86,14 @@ BG_ELIDED_BYTES = {"gbuffer": (None, 1, 1),  # a miss: its mask byte (the slot a
 
 
 def kernel_bytes(name: str, covered_px: float, background_px: float, settings=None) -> float:
+    """Bytes of one launch over covered_px + background_px pixels: the reference kernel's algorithmic
+    bytes (settings None), or what this build's launch must move with background store elision on
+    (settings given: the elided background stores depend on the spatial reuse flags)."""
     if name == "light_merged":  # k_light_merged: the fused direct/emissive pass and the indirect pass in one launch
         return (kernel_bytes("direct_lit_emissive", covered_px, background_px, settings) +
                 kernel_bytes("indirect_lit_ambient", covered_px, background_px, settings))
     c, b = BYTES_PER_PIXEL.get(name, (0, 0))
-    if settings is not None and name in BG_ELIDED_BYTES and os.environ.get("HK_NO_BG_ELIDE") != "1":
+    if settings is not None and name in BG_ELIDED_BYTES:
         flag, alone, with_pair = BG_ELIDED_BYTES[name]
         b = with_pair if flag and getattr(settings, flag) else alone
     return c * covered_px + b * background_px
@@ -271,6 +274,11 @@ def main():
     # rows of this rank (hikari_amd/bands.py): interleaved stripes, or a contiguous band + halo
     stripes = dist_on and use_stripes(cfg["spatial"], cfg["denoise"])
     r = HikariRenderer(device)
+    # HK_BENCH_OPTS="key=value,..." (or "+"-separated): runtime options (hk_set_option) for A/B runs (tools/ab.sh); the
+    # defaults are the tuned configuration
+    bench_opts = {kv.split("=")[0]: float(kv.split("=")[1])
+                  for kv in os.environ.get("HK_BENCH_OPTS", "").replace("+", ",").split(",") if kv}
+    r.set_options(bench_opts)
     r.set_noise()
     r.upload_scene(scene)
     r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
@@ -292,6 +300,10 @@ def main():
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
+    # The band copy and the all-gather run on a communication stream: hk_copy_output_rows on a stream other
+    # than the frame stream waits (device-side) only for the work that produced the plane, and the frame
+    # stream never waits for the copy or the gather, so frame pipelining is kept on every frame.
+    comm = torch.cuda.Stream() if dist_on else None
     # double-buffered band / gathered frame: the all-gather of frame f runs on RCCL's stream
     # while frame f+1 renders; a buffer is reused only after its previous gather completed
     band_t = [torch.zeros((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
@@ -346,23 +358,24 @@ def main():
             r.resolve_accumulation(sp)
         if dist_on:
             k = f & 1
-            if pending[k] is not None:
-                pending[k].wait()  # device-side: the stream waits for that gather
-            if stripes and reorder_done[k] is not None:
-                stream.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
-            r.copy_output_rows(shown, core0, core_rows, band_t[k].data_ptr(), False, sp)
-            if rehearsal:
-                parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
-                dist.all_gather(parts, band_t[k].cpu())
-                full_t[k].copy_(torch.cat(parts))
-            else:
-                pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
+            with torch.cuda.stream(comm):
+                if pending[k] is not None:
+                    pending[k].wait()  # device-side: the comm stream waits for that gather
+                if stripes and reorder_done[k] is not None:
+                    comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
+                r.copy_output_rows(shown, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
+                if rehearsal:
+                    parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
+                    dist.all_gather(parts, band_t[k].cpu())
+                    full_t[k].copy_(torch.cat(parts))
+                else:
+                    pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
             if stripes:
                 with torch.cuda.stream(side):
                     if pending[k] is not None:
                         pending[k].wait()
                     else:
-                        side.wait_stream(stream)
+                        side.wait_stream(comm)
                     torch.index_select(full_t[k], 0, index_t, out=frame_t[k])
                     reorder_done[k] = side.record_event()
 
@@ -371,6 +384,7 @@ def main():
             if pending[k] is not None:
                 pending[k].wait()
                 pending[k] = None
+        torch.cuda.current_stream().wait_stream(comm)
         if stripes:
             torch.cuda.current_stream().wait_stream(side)
 
@@ -404,7 +418,7 @@ def main():
     coverage = float((depth >= np.finfo(np.float32).eps).mean())
     c = r.counters()
     rays = c["traverse_top"] + c["traverse_emitter"]
-    primary = c["primary"]
+    primary = c["primary"] - r.primary_reused()  # rays traced (G-buffer reuse skips static sub-frames)
     if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -416,9 +430,7 @@ def main():
     # per-frame latency: frames alone (frame pipelining off), each bracketed by a device sync
     latency = None
     if world == 1 and not dynamic:
-        lat_env = {"HK_GB_PIPELINE": "0", "HK_DN_PIPELINE": "0"}
-        saved = {k: os.environ.get(k) for k in lat_env}
-        os.environ.update(lat_env)
+        saved = r.set_options({"gbuffer_pipeline": 0, "tail_pipeline": 0})
         r.enable_kernel_timing(False)
         f0 = args.warmup + args.steps
         times = []
@@ -430,19 +442,13 @@ def main():
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t1)
         latency = float(np.median(times)) * 1e3
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        r.set_options(saved)
 
     # after the timed region: a few frames with every kernel alone on the GPU (no channel fork, no
     # frame pipelining), so the roofline can also quote the dominant kernel's isolated duration
     isolated = None
     if world == 1 and spp == 1 and not dynamic:
-        iso_env = {"HK_CHANNEL_STREAMS": "0", "HK_GB_PIPELINE": "0", "HK_DN_PIPELINE": "0"}
-        saved = {k: os.environ.get(k) for k in iso_env}
-        os.environ.update(iso_env)
+        saved = r.set_options({"channel_streams": 0, "gbuffer_pipeline": 0, "tail_pipeline": 0})
         r.set_kernel_timing_interval(1)
         r.enable_kernel_timing(True)
         f0 = args.warmup + args.steps + 10
@@ -451,11 +457,7 @@ def main():
         torch.cuda.synchronize()
         isolated = r.kernel_timing()
         r.enable_kernel_timing(False)
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        r.set_options(saved)
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -473,9 +475,14 @@ def main():
         dom = max(per_frame, key=per_frame.get)
         pix = W * rows
         cov_px, bg_px = pix * coverage, pix * (1.0 - coverage)
-        ref_bytes = int(BYTES_PER_PIXEL.get(dom, (0, 0))[0] * pix)
+        # the reference kernel's algorithmic bytes for this frame: its covered pixels' streams plus its
+        # background pixels' constant stores (BYTES_PER_PIXEL (covered, background); e.g. indirect_lit_ambient
+        # 184 / 220 B).  Round 3 priced every pixel at the covered rate; that figure is kept in diagnostics.
+        ref_bytes = int(kernel_bytes(dom, cov_px, bg_px))
+        r03_bytes = int(BYTES_PER_PIXEL.get(dom, (0, 0))[0] * pix)
         dur = source[dom]
         achieved = ref_bytes / (dur * 1e-3) / 1e9
+        elide = r.get_option("bg_elision") != 0
         # the committed PMC numbers are per launch of a whole 1-GPU frame; a band launch differs
         traffic = load_pmc_traffic(args.config, dom) if world == 1 else None
         result = {
@@ -498,8 +505,9 @@ def main():
             "config": {"workload": cfg["workload"], "resolution": [W, H], "spp": spp,
                        "indirect": "wavefront material-sorted" if wavefront else "megakernel",
                        # background pixels' constant stores skipped where their targets already hold
-                       # them (every buffer keeps the reference's bits; HK_NO_BG_ELIDE=1: off)
-                       "background_store_elision": os.environ.get("HK_NO_BG_ELIDE") != "1",
+                       # them (every buffer keeps the reference's bits; option bg_elision = 0: off)
+                       "background_store_elision": elide,
+                       "options": {k: v for k, v in r.options().items()},
                        "rays_per_frame": int(rays // (args.steps * spp)),
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
@@ -508,8 +516,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "hbm_frac": None if traffic is None else
                          round(traffic / (dur * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "bytes_per_launch": ref_bytes, "bytes_per_pixel": BYTES_PER_PIXEL.get(dom, (0, 0))[0],
-                         "pixels_per_launch": pix, "duration_ms": round(dur, 4),
+                         "bytes_per_launch": ref_bytes, "bytes_per_pixel": list(BYTES_PER_PIXEL.get(dom, (0, 0))),
+                         "pixels_per_launch": pix, "covered_pixels": int(cov_px), "duration_ms": round(dur, 4),
                          "duration": "isolated" if isolated else "in frame (overlapped)"},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
             # each kernel alone on the GPU (the untimed isolated frames after the timed region)
@@ -518,8 +526,11 @@ def main():
             # (background store elision skips constant stores), the share of covered pixels, and all
             # of a frame's compulsory bytes over the frame time
             "diagnostics": {"coverage": round(coverage, 4),
-                            "moved_bytes_per_launch": int(kernel_bytes(dom, cov_px, bg_px, st)),
-                            "frame_compulsory_bytes": int(sum(kernel_bytes(k, cov_px, bg_px, st) *
+                            "moved_bytes_per_launch": int(kernel_bytes(dom, cov_px, bg_px, st if elide else None)),
+                            # round 3's roofline bytes (every pixel at the covered rate) and its fraction
+                            "r03_bytes_per_launch": r03_bytes,
+                            "r03_frac": round(r03_bytes / (dur * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "frame_compulsory_bytes": int(sum(kernel_bytes(k, cov_px, bg_px) *
                                                               launches_per_frame.get(k, 1) for k in timing) * spp)},
         }
         tb = load_traversal_bytes(args.config) if world == 1 and spp == 1 else None

@@ -14,6 +14,7 @@
 // Launch shape: 256-thread workgroups covering a 16x16 pixel tile, each wave an 8x8
 // sub-tile (the reference's workgroup footprint), so rays of one wave stay coherent.
 #include <stdlib.h>
+#include <mutex>
 
 #include "hk_device.h"
 #include "hk_launch.h"
@@ -634,7 +635,7 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
 #ifndef HK_DIRECT_LIT_W4
 #define HK_DIRECT_LIT_W4 1
 #endif
-constexpr size_t DIRECT_LIT_W4_MIN_PX = 400000;
+// (the threshold is LaunchOpts::direct_w4_min_px)
 template <bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_lit_w4(FrameArgs A, ChannelArgs C)
 {
@@ -1725,15 +1726,10 @@ static dim3 tiles(const Frame& F, uint32_t width, int32_t rows) { return tiles(w
 // LDS staging is used when the kernel's scene arrays fit LDS_SCENE_MAX and the kernel gains from
 // it.  Measured on cornell 1080p (1 x MI355X): indirect 0.370 -> 0.317 ms; direct_lit even;
 // direct_emissive 0.167 -> 0.183 ms and the G-buffer even, so those two stay on global loads.
-// HK_LDS_SCENE=0 disables staging, HK_LDS_SCENE=2 stages in every traversal kernel.
-static int lds_mode()
-{
-    const char* e = getenv("HK_LDS_SCENE");  // read per launch (tests switch it in-process)
-    return e ? atoi(e) : 1;
-}
+// Option lds_scene: 0 disables staging, 2 stages in every traversal kernel.
 static uint32_t lds_plan_bytes(const FrameArgs& A, int plan, bool preferred)
 {
-    const int mode = lds_mode();
+    const int mode = A.opt.lds_scene;
     if (mode == 0 || (mode == 1 && !preferred)) return 0u;
     uint32_t b = stage_bytes(A.sc.bytes, plan);
     return b <= LDS_SCENE_MAX ? b : 0u;
@@ -1744,10 +1740,10 @@ void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32
     const uint32_t lds = lds_plan_bytes(A, PLAN_GBUFFER, false);
     const dim3 g = tiles(A.F, A.F.S[0], A.F.S_rows);
     constexpr uint32_t level_bytes = 256u * sizeof(uint2);  // one stack level of the workgroup
-    // HK_GB_STACK_FULL=1: the shallow variant with all GB_STACK_LDS levels (the round-2 allocation)
-    static const bool full = getenv("HK_GB_STACK_FULL") != nullptr;
+    // option gbuffer_stack_full: the shallow variant with all GB_STACK_LDS levels (the round-2 allocation)
+    const bool full = A.opt.gbuffer_stack_full != 0;
     if (lds) hipLaunchKernelGGL((k_gbuffer<true, false>), g, dim3(256), lds, st, A, V, albedo);
-    else if (stack_need <= (uint32_t)GB_STACK_LDS && !getenv("HK_GB_DEEP")) {
+    else if (stack_need <= (uint32_t)GB_STACK_LDS && !A.opt.gbuffer_deep) {
         // pushes never exceed the bound (hk_runtime gb_stack_need: inner nodes on a TLAS + BLAS path)
         const uint32_t levels = full ? (uint32_t)GB_STACK_LDS : (stack_need ? stack_need : 1u);
         hipLaunchKernelGGL((k_gbuffer<false, true>), g, dim3(256), levels * level_bytes, st, A, V, albedo);
@@ -1781,9 +1777,7 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
         else launch_direct_v<true, false, false>(A, C, val, g, 0, st);
     } else {
         const bool val = validation_frame(A.F.number, A.F.direct_validate_interval);
-        const char* wmin = getenv("HK_DIRECT_W4_MIN_PX");  // read per launch: tests force either kernel
-        const double w4_min = wmin ? atof(wmin) : (double)DIRECT_LIT_W4_MIN_PX;
-        if (HK_DIRECT_LIT_W4 && (double)A.F.s[0] * (double)A.F.s_rows >= w4_min) {
+        if (HK_DIRECT_LIT_W4 && (double)A.F.s[0] * (double)A.F.s_rows >= A.opt.direct_w4_min_px) {
             if (lds) {
                 if (val) hipLaunchKernelGGL((k_direct_lit_w4<true, true>), g, dim3(256), lds, st, A, C);
                 else hipLaunchKernelGGL((k_direct_lit_w4<true, false>), g, dim3(256), lds, st, A, C);
@@ -1799,7 +1793,7 @@ template <bool LDS>
 static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, bool vd, bool ve, dim3 g,
                            uint32_t lds, hipStream_t st)
 {
-    static const bool w4 = !getenv("HK_NO_FUSED_W4");
+    const bool w4 = A.opt.fused_w4 != 0;
     if (!LDS && w4 && ve) {
         if (vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
         else hipLaunchKernelGGL((k_direct_fused_w4<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
@@ -1822,27 +1816,34 @@ void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const Channe
 // workgroups of a persistent launch: what the device holds resident of this kernel, at most one 8x8 tile per wave
 static uint32_t persist_grid(const void* kernel, uint32_t lds, const Frame& F)
 {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    }
-    // resident workgroups per CU, per (kernel, LDS bytes): queried once
+    // CU count and resident workgroups per CU, per (device, kernel, LDS bytes): queried once each.
+    // Contexts of different devices may launch from different host threads, so the cache is keyed by
+    // the current device and guarded.
     struct Occ {
+        int dev;
         const void* kernel;
         uint32_t lds;
-        int per_cu;
+        int per_cu, cus;
     };
-    static Occ cache[16];
+    static std::mutex mu;
+    static Occ cache[32];
     static int cached = 0;
-    int per_cu = -1;
-    for (int i = 0; i < cached; ++i)
-        if (cache[i].kernel == kernel && cache[i].lds == lds) per_cu = cache[i].per_cu;
-    if (per_cu < 0) {
-        per_cu = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds);
-        if (cached < 16) cache[cached++] = Occ{kernel, lds, per_cu};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int per_cu = -1, cus = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        for (int i = 0; i < cached; ++i)
+            if (cache[i].dev == dev && cache[i].kernel == kernel && cache[i].lds == lds) {
+                per_cu = cache[i].per_cu;
+                cus = cache[i].cus;
+            }
+        if (per_cu < 0) {
+            per_cu = 0;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds);
+            if (cached < 32) cache[cached++] = Occ{dev, kernel, lds, per_cu, cus};
+        }
     }
     const int32_t rows = F.win_rows > 0 ? F.win_rows : F.s_rows;
     const uint32_t tiles8 = ((F.s[0] + 7u) / 8u) * (((uint32_t)rows + 7u) / 8u);
@@ -1850,16 +1851,11 @@ static uint32_t persist_grid(const void* kernel, uint32_t lds, const Frame& F)
     const uint32_t need = (tiles8 + 3u) / 4u;
     return need < g ? (need > 0u ? need : 1u) : g;
 }
-static bool persist_mode()
-{
-    const char* e = getenv("HK_PERSIST");  // read per launch (tests switch it in-process)
-    return e && e[0] == '1';
-}
 void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipStream_t st)
 {
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, true);
-    if (persist_mode()) {
+    if (A.opt.persistent_indirect) {
 #define HK_PERSIST_LAUNCH(M_, L_)                                                                                    \
     hipLaunchKernelGGL((k_indirect_persist<M_, L_>), dim3(persist_grid((const void*)k_indirect_persist<M_, L_>, lds, A.F)), \
                        dim3(256), lds, st, A, C)
@@ -1887,10 +1883,8 @@ void launch_light_merged(const FrameArgs& A, const ChannelArgs& C0, const Channe
 {
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
     // the indirect workgroups, which live longer, are dispatched first (grid z 0, then the direct ones at
-    // z 1): cornell 8-way stripe 0.1194 -> 0.1181 ms/frame.  HK_MERGE_ORDER=x: even / odd blockIdx.x
-    static const char* order = getenv("HK_MERGE_ORDER");
-    if (order && order[0] == 'x') g.x *= 2u;
-    else g.z = 2u;
+    // z 1): cornell 8-way stripe 0.1194 -> 0.1181 ms/frame against even / odd blockIdx.x
+    g.z = 2u;
     const uint32_t scene = lds_plan_bytes(A, PLAN_LIGHT, true);
     const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
     const bool ve = validation_frame(A.F.number, A.F.emissive_validate_interval);

@@ -10,12 +10,24 @@
 
 namespace hk {
 
+// Kernel-variant choices of the launchers (host only; hk_set_option keys in parentheses).  They pick
+// among bit-identical kernels, so they change speed, never results.
+struct LaunchOpts {
+    int lds_scene = 1;               // ("lds_scene") 0: no LDS scene staging, 1: where it measured faster, 2: every traversal kernel
+    int gbuffer_stack_full = 0;      // ("gbuffer_stack_full") shallow G-buffer walk with all GB_STACK_LDS levels
+    int gbuffer_deep = 0;            // ("gbuffer_deep") the deep-scene G-buffer variant on any scene
+    double direct_w4_min_px = 4e5;   // ("direct_w4_min_px") k_direct_lit_w4 from this many pixels up
+    int fused_w4 = 1;                // ("fused_w4") the 4-wave fused direct/emissive variants
+    int persistent_indirect = 0;     // ("persistent_indirect") k_indirect_persist (opt-in, measured slower)
+};
+
 struct FrameArgs {
     Scene sc;
     Frame F;
     GBuffer G;
     const uchar4* noise;  // 16 x 64 x 64 RGBA8
     Counters cnt;
+    LaunchOpts opt;       // host-side launcher choices (not read by the kernels)
 };
 
 // One channel's bindings: group 5 (variance/render) + group 6 (reservoir pair) of light.rs:455-555.

@@ -33,12 +33,51 @@ struct TimedLaunch {
     const char* name;
     hipEvent_t start, stop;
 };
+
+// Runtime options (hk_set_option / hk_get_option): each picks among schedules or kernel variants that
+// produce the same bits, so they change speed only.  Read once per call from the context (no environment
+// variables on the frame path); the defaults are the measured-fastest configuration.
+enum Opt {
+    OPT_PIPELINE_MIN_PX,     // frame pipelining (G-buffer / tail streams) from this many integrator pixels up
+    OPT_GBUFFER_PIPELINE,    // k_gbuffer of frame f on its own stream next to frame f-1's light passes
+    OPT_TAIL_PIPELINE,       // denoise + tone-sum of frame f on their own stream next to frame f+1
+    OPT_CHANNEL_STREAMS,     // the indirect chain on a side stream next to direct -> emissive
+    OPT_FUSE,                // k_direct_fused when every reprojection is the identity
+    OPT_FUSE_MIN_PX,         // ... from this many pixels up
+    OPT_MERGE,               // k_light_merged: -1 auto (small unpipelined frames), 0 never, 1 whenever possible
+    OPT_BG_ELISION,          // background store elision (bg_elide)
+    OPT_SPATIAL_VIEW,        // spatial view planes written by the indirect temporal pass
+    OPT_BAND_FULL_WINDOWS,   // every pass of a band on all its rows (no per-pass row windows)
+    OPT_LEAF_COLLAPSE,       // leaf-collapsed node copies for the light walks (at scene upload / update)
+    OPT_GBUFFER_REUSE,       // skip k_gbuffer when its slot already holds this frame's planes (static sub-frames)
+    OPT_LDS_SCENE,           // LaunchOpts
+    OPT_GBUFFER_STACK_FULL,
+    OPT_GBUFFER_DEEP,
+    OPT_DIRECT_W4_MIN_PX,
+    OPT_FUSED_W4,
+    OPT_PERSISTENT_INDIRECT,
+    OPT_COUNT
+};
+struct OptDef {
+    const char* key;
+    double def, lo, hi;
+};
+constexpr OptDef OPTS[OPT_COUNT] = {
+    {"pipeline_min_px", 1.2e6, 0.0, 1e12}, {"gbuffer_pipeline", 1, 0, 1},  {"tail_pipeline", 1, 0, 1},
+    {"channel_streams", 1, 0, 1},          {"fuse", 1, 0, 1},              {"fuse_min_px", 1048576.0, 0.0, 1e12},
+    {"merge", -1, -1, 1},                  {"bg_elision", 1, 0, 1},        {"spatial_view_planes", 1, 0, 1},
+    {"band_full_windows", 0, 0, 1},        {"leaf_collapse", 1, 0, 1},     {"gbuffer_reuse", 1, 0, 1},
+    {"lds_scene", 1, 0, 2},                {"gbuffer_stack_full", 0, 0, 1}, {"gbuffer_deep", 0, 0, 1},
+    {"direct_w4_min_px", 4e5, 0.0, 1e12},  {"fused_w4", 1, 0, 1},          {"persistent_indirect", 0, 0, 1},
+};
 }  // namespace
 
 struct hk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string error;
+    double opt[OPT_COUNT];  // hk_set_option
+    bool on(Opt o) const { return opt[o] != 0.0; }
 
     // scene
     void* buf[9] = {};
@@ -136,7 +175,6 @@ struct hk_ctx {
     uint32_t head = 0;                    // frame_number % 2 (PostProcessTextures.head)
     // channel fork-join: emissive and indirect passes on side streams next to direct_lit
     hipStream_t side[2] = {nullptr, nullptr};
-    hipStream_t spacer[8] = {};  // HK_GB_SPACERS / HK_DN_SPACERS experiments (streams without work)
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     // light targets
     uint2* albedo = nullptr;
@@ -178,6 +216,23 @@ struct hk_ctx {
     float* wf_hit_t = nullptr;
     uint32_t* wf_ctl = nullptr;
     uint32_t wf_seg_cap = 0;
+
+    // reads of output planes on streams other than the frame sequence's (hk_copy_output_rows): the plane
+    // and an event after the copy; the next write of that plane waits for it (ext_wait)
+    std::vector<std::pair<const void*, hipEvent_t>> ext_reads;
+    std::vector<hipEvent_t> ext_pool;
+    hipEvent_t ev_frame_mark = nullptr;  // the frame stream's position, waited for by a foreign-stream copy
+    // G-buffer reuse (option gbuffer_reuse): what produced the planes now in each G-buffer slot — the
+    // view, jitter and band window of the k_gbuffer that wrote them and the input generation at that
+    // time (bumped by every scene / texture / instance / size / host-plane / option change)
+    struct GbSig {
+        float view[3 + 16 + 16 + 16 + 2];
+        int32_t win[2];
+        uint64_t gen;
+        bool valid;
+    } gsig[2] = {};
+    uint64_t gen = 1;
+    uint64_t primary_reused = 0;  // primary rays of the skipped launches (since hk_reset_counters)
 
     // timing
     bool timing = false;
@@ -245,6 +300,22 @@ int gb_join(hk_ctx* c, hipStream_t st, bool with_denoise = true)
         return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(denoise) failed");
     return HK_OK;
 }
+// The next write of `plane` (nullptr: of any plane) waits on `st` for the foreign-stream copies that read it.
+int ext_wait(hk_ctx* c, hipStream_t st, const void* plane)
+{
+    for (size_t k = 0; k < c->ext_reads.size();) {
+        if (plane && c->ext_reads[k].first != plane) {
+            ++k;
+            continue;
+        }
+        if (hipStreamWaitEvent(st, c->ext_reads[k].second, 0) != hipSuccess)
+            return fail(c, HK_ERR_HIP, "hipStreamWaitEvent(output read) failed");
+        c->ext_pool.push_back(c->ext_reads[k].second);
+        c->ext_reads[k] = c->ext_reads.back();
+        c->ext_reads.pop_back();
+    }
+    return HK_OK;
+}
 // frame-tail work on dn_stream: it starts after the frame's hk_render_frame (ev_rf) and marks
 // the render / G-buffer slots it read
 int tail_begin(hk_ctx* c)
@@ -275,15 +346,9 @@ int tail_end(hk_ctx* c)
 // (cornell 8-way stripe 0.145 -> 0.172 ms), on a 1080p frame or a 4K band it gains.
 bool pipeline_size(const hk_ctx* c)
 {
-    const char* e = getenv("HK_PIPELINE_MIN_PX");  // read per call: tests switch it per context
-    const double min_px = e ? atof(e) : 1.2e6;
-    return (double)c->s[0] * (double)c->s_rows >= min_px;
+    return (double)c->s[0] * (double)c->s_rows >= c->opt[OPT_PIPELINE_MIN_PX];
 }
-bool dn_pipeline_enabled(const hk_ctx* c)
-{
-    const char* e = getenv("HK_DN_PIPELINE");
-    return (!e || e[0] != '0') && pipeline_size(c);
-}
+bool dn_pipeline_enabled(const hk_ctx* c) { return c->on(OPT_TAIL_PIPELINE) && pipeline_size(c); }
 // the scene, sizes or G-buffer planes change on the caller's stream: the next k_gbuffer must run
 // in caller-stream order (and a synchronous change waits for the one in flight)
 int gb_serialize(hk_ctx* c, bool host_sync)
@@ -560,6 +625,12 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.cnt.emitter = c->counters + COUNTER_SPAN;
     A.cnt.primary = c->counters + 2 * COUNTER_SPAN;
     A.cnt.persist = c->persist;
+    A.opt.lds_scene = (int)c->opt[OPT_LDS_SCENE];
+    A.opt.gbuffer_stack_full = c->on(OPT_GBUFFER_STACK_FULL);
+    A.opt.gbuffer_deep = c->on(OPT_GBUFFER_DEEP);
+    A.opt.direct_w4_min_px = c->opt[OPT_DIRECT_W4_MIN_PX];
+    A.opt.fused_w4 = c->on(OPT_FUSED_W4);
+    A.opt.persistent_indirect = c->on(OPT_PERSISTENT_INDIRECT);
     return A;
 }
 
@@ -575,34 +646,40 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
 // For a static camera every other read is the pixel's own (temporal reprojection is the
 // identity), so the core rows stay bit-identical to the whole frame (test_gpu_row_bands_*),
 // with 1.15x instead of 1.30x the work of an 8-way city 4K band.  Rows outside a pass's window
-// keep stale values that no windowed pass reads.  HK_BAND_FULL_WINDOWS=1: every pass on all rows.
+// keep stale values that no windowed pass reads.  Option band_full_windows: every pass on all rows.
 constexpr int32_t DENOISE_OUT_REACH = 16, SPATIAL_RANGE = 20, EMISSIVE_SPATIAL_RANGE = 10;
 constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
 // Only for a static frame: under camera or instance motion temporal reprojection reads the previous
 // frame's reservoirs at other rows, so every pass runs on the whole band (velocity_zero is set by
-// hk_render_gbuffer before its own window is taken).
+// hk_render_gbuffer before its own window is taken, and cleared by a host G-buffer plane upload).
 FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
 {
     if (c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows || !c->velocity_zero) return A;
-    static const bool full = getenv("HK_BAND_FULL_WINDOWS") && getenv("HK_BAND_FULL_WINDOWS")[0] == '1';
-    if (full) return A;
+    if (c->on(OPT_BAND_FULL_WINDOWS)) return A;
     const int32_t lo = std::max(0, c->core_row0 - margin);
     const int32_t hi = std::min(c->s_rows, c->core_row0 + c->core_rows + margin);
     A.F.win_row0 = lo;
     A.F.win_rows = hi - lo;
     return A;
 }
-// HK_NO_BG_ELIDE=1 switches background store elision off (read per call: tests switch it per context;
-// the G-buffer's and the light passes' masks are both dropped while it is set)
-bool bg_elision_off()
-{
-    const char* e = getenv("HK_NO_BG_ELIDE");
-    return e && e[0] == '1';
-}
+// option bg_elision = 0 switches background store elision off (the G-buffer's and the light passes'
+// masks are both dropped while it is off)
+bool bg_elision_off(const hk_ctx* c) { return !c->on(OPT_BG_ELISION); }
 int32_t light_out_reach(const hk_settings* st) { return st->denoise ? DENOISE_OUT_REACH : 0; }
 int32_t spatial_range(const hk_settings* st)
 {
     return st->indirect_spatial_reuse ? SPATIAL_RANGE : (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0);
+}
+
+// The primary rays a k_gbuffer launch over A counts (its active pixels on the rows it counts: k_gbuffer's
+// n_primary), for the launches G-buffer reuse skips.
+uint64_t gbuffer_primary_rays(const FrameArgs& A)
+{
+    const Frame& F = A.F;
+    const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0, w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : F.S_rows;
+    if (F.stripe_n >= 2) return (uint64_t)F.S[0] * (uint64_t)(w1 - w0);
+    const int32_t lo = std::max(F.S_row0 + w0, F.count_Sy0), hi = std::min(F.S_row0 + w1, F.count_Sy1);
+    return hi > lo ? (uint64_t)F.S[0] * (uint64_t)(hi - lo) : 0u;
 }
 
 int check_ready(hk_ctx* c, bool need_scene)
@@ -656,6 +733,7 @@ int hk_create(int device, hk_ctx** out)
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HK_ERR_NO_DEVICE;
     hk_ctx* c = new hk_ctx();
     c->device = device;
+    for (int k = 0; k < OPT_COUNT; ++k) c->opt[k] = OPTS[k].def;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counters, COUNTER_BYTES) != hipSuccess || hipMemset(c->counters, 0, COUNTER_BYTES) != hipSuccess ||
         hipMalloc(&c->persist, PERSIST_BYTES) != hipSuccess || hipMemset(c->persist, 0, PERSIST_BYTES) != hipSuccess) {
@@ -672,28 +750,20 @@ int hk_create(int device, hk_ctx** out)
             hk_destroy(c);
             return HK_ERR_HIP;
         }
-    // experiment knobs: extra work-free streams created before the G-buffer / tail streams move them
-    // to other hardware queues (the round-robin mapping above)
-    auto spacers = [&](const char* var, int first) {
-        const char* e = getenv(var);
-        const int n = e ? std::min(4, std::max(0, atoi(e))) : 0;
-        for (int k = 0; k < n; ++k) (void)hipStreamCreateWithFlags(&c->spacer[first + k], hipStreamNonBlocking);
-    };
-    spacers("HK_GB_SPACERS", 0);
     if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&c->gb_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gb_call[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_post, hipEventDisableTiming) != hipSuccess ||
-        (spacers("HK_DN_SPACERS", 4), false) ||
         hipStreamCreateWithFlags(&c->dn_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rf, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rslot[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rslot[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gslot[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gslot[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_dn_last, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_dn_last, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_frame_mark, hipEventDisableTiming) != hipSuccess) {
         hk_destroy(c);
         return HK_ERR_HIP;
     }
@@ -728,6 +798,9 @@ void hk_destroy(hk_ctx* c)
         c->event_pool.push_back(t.stop);
     }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    for (auto& r : c->ext_reads) c->ext_pool.push_back(r.second);
+    for (hipEvent_t e : c->ext_pool) (void)hipEventDestroy(e);
+    if (c->ev_frame_mark) (void)hipEventDestroy(c->ev_frame_mark);
     for (int k = 0; k < 2; ++k) {
         if (c->side[k]) (void)hipStreamSynchronize(c->side[k]);
         if (c->side[k]) (void)hipStreamDestroy(c->side[k]);
@@ -740,12 +813,38 @@ void hk_destroy(hk_ctx* c)
     if (c->gb_stream && c->gb_stream != c->side[0]) (void)hipStreamDestroy(c->gb_stream);
     if (c->dn_stream && c->dn_stream != c->side[0]) (void)hipStreamDestroy(c->dn_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    for (hipStream_t& sp : c->spacer)
-        if (sp) (void)hipStreamDestroy(sp);
     delete c;
 }
 
 const char* hk_last_error(const hk_ctx* c) { return c ? c->error.c_str() : "null context"; }
+
+int hk_set_option(hk_ctx* c, const char* key, double value)
+{
+    if (!c || !key) return HK_ERR_INVALID;
+    for (int k = 0; k < OPT_COUNT; ++k) {
+        if (std::strcmp(OPTS[k].key, key) != 0) continue;
+        if (!(value >= OPTS[k].lo && value <= OPTS[k].hi))
+            return fail(c, HK_ERR_INVALID, std::string("option ") + key + " out of range");
+        c->opt[k] = value;
+        c->gen++;  // (G-buffer reuse: planes written under other options are not reused)
+        if (k == OPT_BAND_FULL_WINDOWS) c->bg_valid[0] = c->bg_valid[1] = c->gb_valid = false;  // new windows
+        return HK_OK;
+    }
+    return fail(c, HK_ERR_INVALID, std::string("unknown option ") + key);
+}
+
+int hk_get_option(const hk_ctx* c, const char* key, double* value)
+{
+    if (!c || !key || !value) return HK_ERR_INVALID;
+    for (int k = 0; k < OPT_COUNT; ++k)
+        if (std::strcmp(OPTS[k].key, key) == 0) {
+            *value = c->opt[k];
+            return HK_OK;
+        }
+    return HK_ERR_INVALID;
+}
+
+const char* hk_option_name(int index) { return index >= 0 && index < OPT_COUNT ? OPTS[index].key : nullptr; }
 
 int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
 {
@@ -759,6 +858,7 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
                             sizeof(hk_emissive)};
     if (d->instances.count == 0 || d->materials.count == 0)
         return fail(c, HK_ERR_INVALID, "scene needs at least one instance and one material");
+    c->gen++;
     for (int i = 0; i < 9; ++i)
         if (arr[i]->count && !arr[i]->data) return fail(c, HK_ERR_INVALID, "scene array with count but no data");
     HK_HIP(c, hipStreamSynchronize(c->stream));
@@ -839,7 +939,7 @@ int hk_scene_upload(hk_ctx* c, const hk_scene_desc* d)
                              c->stream));
     HK_HIP(c, hipMemcpyAsync(c->walk_nodes[1], c->buf[5], (size_t)n_tlas * sizeof(hk_node), hipMemcpyDeviceToDevice,
                              c->stream));
-    if (!getenv("HK_NO_COLLAPSE")) {
+    if (c->on(OPT_LEAF_COLLAPSE)) {
         launch_collapse_leaves(c->walk_nodes[0], n_blas, d_aux + n_blas, d_aux + 2 * (size_t)n_blas, c->collapse_scratch,
                                c->stream);
         launch_collapse_leaves(c->walk_nodes[1], n_tlas, nullptr, nullptr, c->collapse_scratch, c->stream);
@@ -868,6 +968,7 @@ int hk_update_instances(hk_ctx* c, const float* models, const float* local_aabbs
     hipStream_t st = pick(c, stream);
     HK_TRY(gb_join(c, st));
     HK_TRY(gb_serialize(c, false));
+    c->gen++;
     const uint32_t n = count, m = c->count[8], n_alias = c->count[3];
     const uint32_t nm = n > m ? n : m;
     auto align = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -918,7 +1019,7 @@ int hk_update_instances(hk_ctx* c, const float* models, const float* local_aabbs
         launch_build_wide((const hk_node*)c->buf[5], c->count[5], nullptr, nullptr, c->tlas_wide, st);
         (void)hipMemcpyAsync(c->walk_nodes[1], c->buf[5], (size_t)c->count[5] * sizeof(hk_node), hipMemcpyDeviceToDevice,
                              st);
-        if (!getenv("HK_NO_COLLAPSE"))
+        if (c->on(OPT_LEAF_COLLAPSE))
             launch_collapse_leaves(c->walk_nodes[1], c->count[5], nullptr, nullptr, c->collapse_scratch, st);
     });
     HK_HIP(c, hipGetLastError());
@@ -953,6 +1054,7 @@ int hk_texture_upload(hk_ctx* c, const hk_texture* t, uint32_t count)
     HK_TRY(gb_serialize(c, true));
     std::vector<hk_texture_desc> desc(count);
     uint64_t total = 0;
+    c->gen++;
     for (uint32_t i = 0; i < count; ++i) {
         if (!t[i].width || !t[i].height || !t[i].rgba8) return fail(c, HK_ERR_INVALID, "texture without texels");
         if (t[i].format > HK_TEXTURE_RGBA8_UNORM || t[i].address_u > HK_ADDRESS_MIRROR_REPEAT ||
@@ -1036,6 +1138,7 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     HK_HIP(c, hipStreamSynchronize(c->gb_stream));
     HK_HIP(c, hipStreamSynchronize(c->dn_stream));
     free_targets(c);
+    c->gen++;
     c->albedo_fresh = false;
     c->S[0] = width;
     c->S[1] = height;
@@ -1141,6 +1244,7 @@ int hk_set_band_halo(hk_ctx* c, uint32_t rows)
     if (!c || rows > 4096) return HK_ERR_INVALID;
     c->halo = (int32_t)rows;
     c->bg_valid[0] = c->bg_valid[1] = false;
+    c->gen++;
     return HK_OK;
 }
 
@@ -1169,13 +1273,34 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     // passes, denoise, tone-sum, readbacks) and a post-process of frame f-1 (it reads the previous
     // slot); k_gbuffer waits for exactly those on gb_stream and so overlaps frame f-1's light
     // passes.  A scene / size / plane change since the last call serialises it instead.
-    const char* gp = getenv("HK_GB_PIPELINE");
-    const bool pipeline = !gp || gp[0] != '0';
+    const bool pipeline = c->on(OPT_GBUFFER_PIPELINE);
     // Event markers are recorded only on the pipelined path: each one between two kernels of a stream
     // costs it ~6 us (cornell 8-way stripe, where the serial frame is 3 kernels), and the serial path
     // has no other stream waiting on them.
     const uint32_t e = c->gb_calls & 1u;
     hipStream_t gs = st;
+    // G-buffer reuse: the slot this frame's planes go to (the other one) already holds exactly them when the
+    // k_gbuffer that wrote it saw the same view, jitter and band window, nothing it reads changed since
+    // (generation) and nothing moved (no motion vectors: the velocity plane is zero in both).  The planes
+    // then stay as they are, bit for bit what a new trace would store (the 16
+    // sub-frames of a displayed frame share camera and scene).  Only the primary-ray counter differs: it
+    // counts rays traced.
+    hk_ctx::GbSig sig;
+    std::memset(&sig, 0, sizeof(sig));
+    {
+        float* v = sig.view;
+        for (int i = 0; i < 3; ++i) *v++ = in->view.world_position[i];
+        for (int i = 0; i < 16; ++i) *v++ = in->view.view_proj[i];
+        for (int i = 0; i < 16; ++i) *v++ = in->view.inverse_view_proj[i];
+        for (int i = 0; i < 16; ++i) *v++ = in->has_previous_view ? in->previous_view_proj[i] : in->view.view_proj[i];
+        *v++ = in->view.projection[15];
+        *v++ = (float)in->jitter;
+        sig.gen = c->gen;
+        sig.valid = true;
+    }
+    const bool jitter_static = in->jitter == HK_JITTER_NONE;
+    const bool still = !c->models_dirty &&
+                       std::memcmp(sig.view + 3, sig.view + 3 + 32, 16 * sizeof(float)) == 0;  // previous view = view
     const bool pipe = pipeline && pipeline_size(c) && !c->gb_serial && c->gb_calls > 0;
     c->entry_other[e] = c->other_picks;
     c->entry_epoch[e] = c->frame_st_epoch;
@@ -1184,6 +1309,35 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
                         c->frame_st_epoch == c->rf_epoch;
     c->gb_tail_seq = 0;
     c->gb_wait_valid = false;
+    {
+        const uint32_t next = c->gslot ^ 1u;  // the slot this frame's planes go to
+        FrameArgs W = pass_window(c, frame_args(c, nullptr, in), GBUFFER_REACH);
+        sig.win[0] = W.F.win_row0;
+        sig.win[1] = W.F.win_rows;
+        const hk_ctx::GbSig& have = c->gsig[next];
+        if (c->on(OPT_GBUFFER_REUSE) && still && jitter_static && have.valid && c->velocity_zero &&
+            c->albedo_fresh && have.gen == sig.gen && have.win[0] == sig.win[0] &&
+            have.win[1] == sig.win[1] && std::memcmp(have.view, sig.view, sizeof(sig.view)) == 0 && !c->gb_serial && c->gb_calls > 0) {
+            // (the previous frame's G-buffer came from k_gbuffer too — albedo_fresh, velocity_zero — so both
+            // slots hold traced planes of a still camera)
+            std::swap(c->g_position, c->g_prev_position);
+            std::swap(c->g_velocity_uv, c->g_prev_velocity_uv);
+            std::swap(c->g_normal, c->g_prev_normal);
+            std::swap(c->g_depth_gradient, c->g_prev_depth_gradient);
+            std::swap(c->g_instance_material, c->g_prev_instance_material);
+            std::swap(c->albedo, c->albedo_prev);
+            c->gslot = next;
+            c->head = in->frame_number & 1u;
+            c->timing_frame = in->frame_number % c->timing_every == 0u;
+            // (post_pending stays: a post-process read both slots, and the next launch overwrites one)
+            // no launch to reason about: the next hk_render_frame records its fork marker
+            c->gb_call_rec = false;
+            c->gb_on_gs = false;
+            c->gb_calls++;
+            c->primary_reused += gbuffer_primary_rays(W);
+            return HK_OK;
+        }
+    }
     if (pipe) {
         HK_HIP(c, hipEventRecord(c->ev_gb_call[e], st));
         gs = c->gb_stream;
@@ -1252,7 +1406,7 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
     A = pass_window(c, A, GBUFFER_REACH);
     V.bg = nullptr;
     V.bg_need = 0;
-    if (bg_elision_off()) {
+    if (bg_elision_off(c)) {
         c->gb_valid = false;  // the mask is rebuilt from zero when elision is switched back on
     } else {
         if (!c->gb_valid || c->gb_key[0] != A.F.win_row0 || c->gb_key[1] != A.F.win_rows) {
@@ -1264,7 +1418,14 @@ int hk_render_gbuffer(hk_ctx* c, const hk_frame_inputs* in, void* stream)
         V.bg = c->gbmask;
         V.bg_need = 1u << c->gslot;  // the planes' physical slot (swapped with gslot above)
     }
+    for (const void* plane : {(const void*)c->g_position, (const void*)c->g_velocity_uv, (const void*)c->g_normal,
+                              (const void*)c->g_depth_gradient, (const void*)c->g_instance_material, (const void*)c->albedo})
+        HK_TRY(ext_wait(c, gs, plane));
     timed(c, "gbuffer", gs, [&] { launch_gbuffer(A, V, c->albedo, c->gb_stack_need, gs); });
+    sig.win[0] = A.F.win_row0;
+    sig.win[1] = A.F.win_rows;
+    sig.valid = V.motion == 0;
+    c->gsig[c->gslot] = sig;
     if (c->models_dirty) {  // this frame's models become the next frame's previous ones
         HK_HIP(c, hipMemcpy2DAsync(c->prev_models, 64, (const char*)c->buf[4] + offsetof(hk_instance, model),
                                    sizeof(hk_instance), 64, c->count[4], hipMemcpyDeviceToDevice, gs));
@@ -1300,7 +1461,11 @@ int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, i
     default: return fail(c, HK_ERR_INVALID, "unknown G-buffer plane");
     }
     if (bytes != need) return fail(c, HK_ERR_INVALID, "G-buffer plane size mismatch");
+    c->gen++;
     c->gb_valid = false;  // host planes: the G-buffer elision mask no longer describes the slots
+    // host planes may carry any velocity: the identity-reprojection paths (fused launch, band row windows,
+    // the direct pair's elision) stay off until the next k_gbuffer of a static frame
+    c->velocity_zero = false;
     // a new frame's position / velocity plane: the current one becomes the previous (prepass.rs:309-317)
     if (plane == 0) {
         std::swap(c->g_position, c->g_prev_position);
@@ -1312,6 +1477,7 @@ int hk_set_gbuffer_plane(hk_ctx* c, int plane, const void* data, size_t bytes, i
     (void)hipSetDevice(c->device);
     hipStream_t st = pick(c, stream);
     HK_TRY(gb_join(c, st));
+    HK_TRY(ext_wait(c, st, dst));
     c->gb_serial = true;
     HK_HIP(c, hipMemcpyAsync(dst, data, bytes, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
     if (!device_ptr) HK_HIP(c, hipStreamSynchronize(st));
@@ -1344,7 +1510,7 @@ static int bg_mask(hk_ctx* c, int k, const FrameArgs& A, bool use, bool pair, hi
 {
     C.bg = nullptr;
     C.bg_need = 0;
-    if (!use || bg_elision_off()) {
+    if (!use || bg_elision_off(c)) {
         c->bg_valid[k] = false;
         return HK_OK;
     }
@@ -1394,6 +1560,17 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (slot_wait && !slot_covered) HK_HIP(c, hipStreamWaitEvent(st, c->ev_rslot[c->rslot], 0));
     // (k_albedo rewrites the albedo plane a previous tail may still read: full join then)
     HK_TRY(gb_join(c, st, !swap || !c->albedo_fresh));
+    // foreign-stream copies of the planes this call writes wait on st; when the indirect chain's own planes
+    // are among them, its side stream must fork from st after those waits (no fork shortcut below)
+    bool had_ext = false;
+    for (const auto& r : c->ext_reads) had_ext |= r.first == c->render[2] || r.first == c->variance[2];
+    if (!c->ext_reads.empty()) {
+        HK_TRY(ext_wait(c, st, c->albedo));
+        for (int ch = 0; ch < 3; ++ch) {
+            HK_TRY(ext_wait(c, st, c->render[ch]));
+            HK_TRY(ext_wait(c, st, c->variance[ch]));
+        }
+    }
     c->rf_swapped = swap;
     c->tail_open = false;
     if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
@@ -1407,9 +1584,8 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // before returning.  The latency-bound traversal kernels leave issue slots and memory-level
     // parallelism idle, so the overlap pays even when one pass fills the GPU (cornell 1080p
     // 0.81 -> 0.77 ms/frame; 64x64 0.26 -> 0.18 ms).  Per-kernel event timings then include the
-    // overlap.  HK_CHANNEL_STREAMS=0 restores the serial order.
-    bool fork = true;
-    if (const char* e = getenv("HK_CHANNEL_STREAMS")) fork = e[0] == '1';
+    // overlap.  Option channel_streams = 0 restores the serial order.
+    const bool fork = c->on(OPT_CHANNEL_STREAMS);
     // fork_events: the indirect chain really runs on the side stream (not when k_light_merged takes it)
     bool fork_events = false;
     hipStream_t s1 = st, s2 = fork ? c->side[1] : st;
@@ -1428,12 +1604,9 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // instance motion: velocity_zero; host planes may hold any velocity) at upscale ratio 1 (the
     // deferred jitter is the identity).  Only for frames of >= 1 Mpx: there it saves a launch and a
     // tail (cornell 1080p 0.652 -> 0.622 ms); on a small band (a 4- or 8-way split) the two passes
-    // on their own overlap the indirect chain better (0.143 vs 0.151 ms).  HK_FUSE_MIN_PX overrides
-    // the size threshold (tests).
-    const char* fmin = getenv("HK_FUSE_MIN_PX");
-    const double fuse_min_px = fmin ? atof(fmin) : (double)(1u << 20);
+    // on their own overlap the indirect chain better (0.143 vs 0.151 ms).  Options fuse, fuse_min_px.
     const bool fuse = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f &&
-                      (double)c->s[0] * (double)c->s_rows >= fuse_min_px && !getenv("HK_NO_FUSE");
+                      (double)c->s[0] * (double)c->s_rows >= c->opt[OPT_FUSE_MIN_PX] && c->on(OPT_FUSE);
     // background elision (bg_mask, hk_kernels.hip bg_elide); the separate launches share the pair's mask
     // (direct_pass).  A background pixel's own targets (temporal record, render, variance) are written by
     // that pixel alone, so they elide with or without motion.  Under motion the temporal passes also scatter
@@ -1449,9 +1622,8 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // spatial view planes (ChannelArgs::view): the indirect temporal pass writes them next to the records
     // it stores, this frame's spatial pass reads its neighbours from them.  Only when that temporal pass
     // stores its records (temporal_reuse; otherwise `cur` keeps older records the planes do not mirror).
-    // HK_NO_SP_VIEW=1: off (the spatial pass gathers the records' own planes).
-    const char* nv = getenv("HK_NO_SP_VIEW");
-    if (settings->indirect_spatial_reuse && settings->temporal_reuse && !(nv && nv[0] == '1')) {
+    // Option spatial_view_planes = 0: off (the spatial pass gathers the records' own planes).
+    if (settings->indirect_spatial_reuse && settings->temporal_reuse && c->on(OPT_SPATIAL_VIEW)) {
         C2.view = c->sp_view;
         C2.view_n = c->res_n;
     }
@@ -1467,13 +1639,12 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // 0.263, 4-way 0.164 -> 0.160, 8-way 0.144 -> 0.112 ms/frame with the serial path's event
     // elision); on pipelined frames the streams overlap better (1080p 0.472 vs 0.486, city 4K 6.25
     // vs 7.21: spatial reuse would wait for the direct pass).  Not in the isolated-kernel measurement
-    // mode (HK_CHANNEL_STREAMS=0).  HK_MERGE=1: whenever possible, 0: never.
-    const char* me = getenv("HK_MERGE");
-    const bool merge_possible = identity && fork && !multi && !wf && !light_lds_direct(A) && !getenv("HK_NO_FUSE");
+    // mode (channel_streams = 0).  Option merge: 1 whenever possible, 0 never, -1 this default.
+    const bool merge_possible = identity && fork && !multi && !wf && !light_lds_direct(A) && c->on(OPT_FUSE);
     const bool merge_default = !pipeline_size(c) && !settings->indirect_spatial_reuse && !settings->emissive_spatial_reuse;
-    const bool merge = merge_possible && (me ? me[0] == '1' : merge_default);
+    const bool merge = merge_possible && (c->opt[OPT_MERGE] < 0.0 ? merge_default : c->on(OPT_MERGE));
     if (fork && !merge) {
-        if (gb_fresh && c->rf_side_only && swap && c->albedo_fresh) {
+        if (gb_fresh && c->rf_side_only && swap && c->albedo_fresh && !had_ext) {
             // The fork marker would make the side stream wait for the caller stream here.  What the
             // indirect chain reads of that stream's work: the work before W (k_gbuffer waited for it),
             // frame f-1's hk_render_frame (its indirect chain ran on the side stream itself; the rest of
@@ -1553,6 +1724,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     hipStream_t st = async ? c->dn_stream : caller;
     if (async) HK_TRY(tail_begin(c));
     else HK_TRY(gb_join(c, st));
+    for (int ch = 0; ch < 3; ++ch) HK_TRY(ext_wait(c, st, c->denoised[ch]));
     FrameArgs A = frame_args(c, settings, in);
     int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
     DenoiseArgs D;
@@ -1600,6 +1772,7 @@ int hk_tone_sum(hk_ctx* c, const hk_settings* settings, void* stream)
     T.emissive = settings->denoise ? c->denoised[1] : c->render[1];
     T.indirect = settings->indirect_bounces == 0u ? nullptr : (settings->denoise ? c->denoised[2] : c->render[2]);
     T.output = c->tone_buf[c->head];
+    HK_TRY(ext_wait(c, st, T.output));
     timed(c, "tone_mapping", st, [&] { launch_tone(A, T, st); });
     if (async) HK_TRY(tail_end(c));
     HK_HIP(c, hipGetLastError());
@@ -1617,6 +1790,8 @@ int hk_post_process(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in,
     HK_TRY(gb_join(c, s));
     c->head = in->frame_number & 1u;
     const uint32_t head = c->head;
+    HK_TRY(ext_wait(c, s, c->upscale));
+    HK_TRY(ext_wait(c, s, c->taa_buf[head]));
     // post_process.rs:663-731 sizes: ceil(S * scale), scale = 1 / ratio, x 2 after SMAA TU4x
     float scale = 1.0f / c->ratio;
     const bool smaa = st->upscale == 0u, taa = st->taa == 0u;
@@ -1674,13 +1849,18 @@ int hk_post_process(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in,
     return HK_OK;
 }
 
+// Sub-frame accumulation is part of the frame sequence: after a slot-swapping hk_render_frame it runs in
+// the frame's tail on dn_stream (after the tone-sum it reads), next to the following sub-frame's light
+// passes; otherwise on the caller's stream.  Only these two calls touch the accumulator.
 int hk_accumulate(hk_ctx* c, int reset, void* stream)
 {
     int rc = check_ready(c, false);
     if (rc) return rc;
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
-    HK_TRY(gb_join(c, st));
+    const bool async = c->rf_swapped && c->tail_open;  // this frame's tone-sum ran in the tail
+    hipStream_t st = async ? c->dn_stream : pick_frame(c, stream);
+    if (async) HK_TRY(tail_begin(c));
+    else HK_TRY(gb_join(c, st));
     const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
     if (!c->accum) {
         HK_HIP(c, hipMalloc(&c->accum, n * sizeof(float4)));
@@ -1690,6 +1870,7 @@ int hk_accumulate(hk_ctx* c, int reset, void* stream)
     }
     if (reset) c->accum_n = 0;
     timed(c, "accumulate", st, [&] { launch_accumulate(c->tone_buf[c->head], c->accum, (uint32_t)n, reset, st); });
+    if (async) HK_TRY(tail_end(c));
     HK_HIP(c, hipGetLastError());
     c->accum_n += 1;
     return HK_OK;
@@ -1701,10 +1882,14 @@ int hk_resolve_accumulation(hk_ctx* c, void* stream)
     if (rc) return rc;
     if (!c->accum || c->accum_n == 0) return fail(c, HK_ERR_STATE, "nothing accumulated (hk_accumulate)");
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
-    HK_TRY(gb_join(c, st));
+    const bool async = c->rf_swapped && c->tail_open;
+    hipStream_t st = async ? c->dn_stream : pick_frame(c, stream);
+    if (async) HK_TRY(tail_begin(c));
+    else HK_TRY(gb_join(c, st));
+    HK_TRY(ext_wait(c, st, c->accum_out));
     const size_t n = (size_t)c->s[0] * (size_t)c->s_rows;
     timed(c, "resolve", st, [&] { launch_resolve(c->accum, (uint32_t)n, (float)c->accum_n, c->accum_out, st); });
+    if (async) HK_TRY(tail_end(c));
     HK_HIP(c, hipGetLastError());
     return HK_OK;
 }
@@ -1804,12 +1989,38 @@ int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* d
     if (!p) return fail(c, HK_ERR_INVALID, "unknown output id");
     if (row0 + rows > h) return fail(c, HK_ERR_INVALID, "row range outside the plane");
     (void)hipSetDevice(c->device);
-    hipStream_t st = pick(c, stream);
+    // A copy on a stream other than the frame sequence's (a communication stream) enqueues nothing on the
+    // frame stream but, when the plane's producer may have run there, an event marker: the frame stream
+    // never waits for the copy, and the plane's next writer waits for it (ext_reads).  The tone-mapped,
+    // accumulated and denoised planes of a pipelined frame come from its tail (dn_stream, ev_dn_last).
+    const hipStream_t given = stream ? (hipStream_t)stream : c->stream;
+    const bool foreign = c->frame_st && given != c->frame_st && !to_host;
+    hipStream_t st = foreign ? given : pick(c, stream);
     HK_TRY(gb_join(c, st));
+    if (foreign) {
+        const bool from_tail = c->rf_swapped && c->tail_open &&
+                               (id == HK_OUT_TONE_MAPPED || id == HK_OUT_ACCUMULATED ||
+                                (id >= HK_OUT_DENOISED_DIRECT && id <= HK_OUT_DENOISED_INDIRECT));
+        if (!from_tail) {
+            HK_HIP(c, hipEventRecord(c->ev_frame_mark, c->frame_st));
+            HK_HIP(c, hipStreamWaitEvent(st, c->ev_frame_mark, 0));
+        }
+    }
     size_t pitch = (size_t)w * b;
     HK_HIP(c, hipMemcpyAsync(dst, (const char*)p + (size_t)row0 * pitch, (size_t)rows * pitch,
                              to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
     if (to_host) HK_HIP(c, hipStreamSynchronize(st));
+    if (foreign) {
+        hipEvent_t e = nullptr;
+        if (!c->ext_pool.empty()) {
+            e = c->ext_pool.back();
+            c->ext_pool.pop_back();
+        } else {
+            HK_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        HK_HIP(c, hipEventRecord(e, st));
+        c->ext_reads.emplace_back(p, e);
+    }
     return HK_OK;
 }
 
@@ -1858,6 +2069,7 @@ int hk_reset_counters(hk_ctx* c, void* stream)
     (void)hipSetDevice(c->device);
     HK_TRY(gb_join(c, pick(c, stream)));
     HK_HIP(c, hipMemsetAsync(c->counters, 0, COUNTER_BYTES, pick(c, stream)));
+    c->primary_reused = 0;
     return HK_OK;
 }
 
@@ -1875,7 +2087,8 @@ int hk_read_counters(hk_ctx* c, hk_counters* out, void* stream)
         for (size_t i = 0; i < COUNTER_SHARDS; ++i) sum[k] += v[k * COUNTER_SPAN + i * COUNTER_STRIDE];
     out->traverse_top = sum[0];
     out->traverse_emitter = sum[1];
-    out->primary = sum[2];
+    out->primary = sum[2] + c->primary_reused;
+    out->primary_reused = c->primary_reused;
     return HK_OK;
 }
 

@@ -106,7 +106,8 @@ class hk_frame_inputs(C.Structure):
 
 
 class hk_counters(C.Structure):
-    _fields_ = [("traverse_top", C.c_uint64), ("traverse_emitter", C.c_uint64), ("primary", C.c_uint64)]
+    _fields_ = [("traverse_top", C.c_uint64), ("traverse_emitter", C.c_uint64), ("primary", C.c_uint64),
+                ("primary_reused", C.c_uint64)]
 
 
 # std430 record sizes (include/hk_types.h)
@@ -137,6 +138,9 @@ def lib() -> C.CDLL:
         "hk_destroy": (None, [vp]),
         "hk_last_error": (C.c_char_p, [vp]),
         "hk_settings_default": (None, [C.POINTER(hk_settings)]),
+        "hk_set_option": (i32, [vp, C.c_char_p, C.c_double]),
+        "hk_get_option": (i32, [vp, C.c_char_p, C.POINTER(C.c_double)]),
+        "hk_option_name": (C.c_char_p, [i32]),
         "hk_scene_upload": (i32, [vp, C.POINTER(hk_scene_desc)]),
         "hk_set_noise": (i32, [vp, vp, u32, u32]),
         "hk_texture_upload": (i32, [vp, vp, u32]),
@@ -191,7 +195,8 @@ def lib() -> C.CDLL:
 
 # symbols include/*.h declare (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
-    "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_scene_upload",
+    "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_set_option",
+    "hk_get_option", "hk_option_name", "hk_scene_upload",
     "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_sync", "hk_set_wavefront", "hk_lane_stats", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing", "hk_set_kernel_timing_interval",

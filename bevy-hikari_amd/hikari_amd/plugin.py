@@ -42,7 +42,11 @@ def _check(ctx, rc: int, what: str) -> None:
 class HikariRenderer:
     """A camera's integrator context (hk_ctx)."""
 
-    def __init__(self, device: int = 0):
+    # options (hk_set_option) applied to every context this class creates; tests use it to force kernel
+    # variants and schedules for all the contexts of a test (tests/conftest.py `hk_options`)
+    defaults: dict = {}
+
+    def __init__(self, device: int = 0, options: Optional[dict] = None):
         L = _abi.lib()
         h = C.c_void_p()
         rc = L.hk_create(device, C.byref(h))
@@ -51,6 +55,8 @@ class HikariRenderer:
         self._L = L
         self.ctx = h.value
         self.width = self.height = 0
+        for k, v in {**self.defaults, **(options or {})}.items():
+            self.set_option(k, v)
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -59,6 +65,32 @@ class HikariRenderer:
 
     def __del__(self):
         self.close()
+
+    # ---- runtime options (hk_set_option): schedule / kernel-variant choices, results unchanged
+    def set_option(self, key: str, value: float) -> None:
+        _check(self.ctx, self._L.hk_set_option(self.ctx, key.encode(), float(value)), f"hk_set_option({key})")
+
+    def get_option(self, key: str) -> float:
+        v = C.c_double()
+        _check(self.ctx, self._L.hk_get_option(self.ctx, key.encode(), C.byref(v)), f"hk_get_option({key})")
+        return v.value
+
+    def options(self) -> dict:
+        """{key: value} of every option of this context."""
+        out, i = {}, 0
+        while True:
+            k = self._L.hk_option_name(i)
+            if k is None:
+                return out
+            out[k.decode()] = self.get_option(k.decode())
+            i += 1
+
+    def set_options(self, opts: dict) -> dict:
+        """Set several options; returns their previous values (for restoring)."""
+        old = {k: self.get_option(k) for k in opts}
+        for k, v in opts.items():
+            self.set_option(k, v)
+        return old
 
     # ---- resources
     def upload_scene(self, scene: Scene) -> None:
@@ -191,6 +223,13 @@ class HikariRenderer:
         c = _abi.hk_counters()
         _check(self.ctx, self._L.hk_read_counters(self.ctx, C.byref(c), None), "hk_read_counters")
         return {"traverse_top": c.traverse_top, "traverse_emitter": c.traverse_emitter, "primary": c.primary}
+
+    def primary_reused(self) -> int:
+        """Primary rays (included in counters()["primary"]) of frames whose G-buffer planes were reused
+        rather than traced (option gbuffer_reuse)."""
+        c = _abi.hk_counters()
+        _check(self.ctx, self._L.hk_read_counters(self.ctx, C.byref(c), None), "hk_read_counters")
+        return c.primary_reused
 
     def enable_kernel_timing(self, enable: bool = True) -> None:
         _check(self.ctx, self._L.hk_enable_kernel_timing(self.ctx, int(enable)), "hk_enable_kernel_timing")

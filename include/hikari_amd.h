@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HK_ABI_VERSION 2
+#define HK_ABI_VERSION 3
 
 enum {
     HK_OK = 0,
@@ -180,15 +180,46 @@ typedef enum hk_output_id {
 typedef struct hk_counters {
     uint64_t traverse_top;      /* traverse_top calls (light.wgsl:442) */
     uint64_t traverse_emitter;  /* emitter traverse_bottom calls in select_light_candidate (light.wgsl:687) */
-    uint64_t primary;           /* primary rays of hk_render_gbuffer */
+    uint64_t primary;           /* primary rays of hk_render_gbuffer: one per pixel per frame */
+    uint64_t primary_reused;    /* of those, the rays of frames whose planes were reused (option gbuffer_reuse), not traced */
 } hk_counters;
 
 /* ---- lifetime ---- */
 int hk_abi_version(void);
+/* Tuned configuration: the context creates its streams in a fixed order (caller
+ * stream, two side streams — one carries no work, it only shifts the next ones — G-buffer stream,
+ * tail stream), and HIP maps streams round-robin onto the process's hardware queues.  The defaults of
+ * hk_set_option were measured with HIP's default GPU_MAX_HW_QUEUES=4; more queues let every stream
+ * run concurrently and measured slower (cornell 1080p 0.58 -> 0.70 ms/frame). */
 int hk_create(int device, hk_ctx** out_ctx);
 void hk_destroy(hk_ctx* ctx);
 const char* hk_last_error(const hk_ctx* ctx);
 void hk_settings_default(hk_settings* out);
+
+/* Runtime options of a context (no reference counterpart: the reference has one schedule).  Every
+ * option chooses among schedules or kernel variants that produce the same bits, so results never
+ * depend on them; the defaults are the measured-fastest configuration.  Nothing is read from the
+ * environment.  Keys (default):
+ *   pipeline_min_px (1.2e6)  frame pipelining from this many integrator pixels up
+ *   gbuffer_pipeline (1)     frame f's G-buffer on its own stream next to frame f-1's light passes
+ *   tail_pipeline (1)        frame f's denoise / tone-sum / accumulation next to frame f+1's light passes
+ *   channel_streams (1)      the indirect chain on a side stream next to direct -> emissive
+ *   fuse (1), fuse_min_px (2^20)  direct_lit + emissive in one launch (identity reprojection only)
+ *   merge (-1)               direct + indirect in one launch: -1 small unpipelined frames, 0 never, 1 always
+ *   bg_elision (1)           skip background stores whose targets already hold their constant words
+ *   spatial_view_planes (1)  the indirect temporal pass writes spatial reuse's neighbour view planes
+ *   band_full_windows (0)    a band runs every pass on all its rows (no per-pass row windows)
+ *   leaf_collapse (1)        leaf-collapsed node copies for the light walks (applied at the next upload)
+ *   gbuffer_reuse (1)        skip the G-buffer trace when its slot already holds this frame's planes
+ *                            (static camera, jitter and instances: the sub-frames of an accumulation)
+ *   lds_scene (1)            0 no LDS scene staging, 1 where measured faster, 2 every traversal kernel
+ *   gbuffer_stack_full (0), gbuffer_deep (0), direct_w4_min_px (4e5), fused_w4 (1),
+ *   persistent_indirect (0)  kernel-variant choices (tests force each variant with them)
+ * hk_set_option returns HK_ERR_INVALID for an unknown key or a value outside the key's range. */
+int hk_set_option(hk_ctx* ctx, const char* key, double value);
+int hk_get_option(const hk_ctx* ctx, const char* key, double* value);
+/* key of option `index` (0, 1, ...; NULL past the last one) */
+const char* hk_option_name(int index);
 
 /* ---- resources ---- */
 int hk_scene_upload(hk_ctx* ctx, const hk_scene_desc* scene);
@@ -294,7 +325,10 @@ int hk_sync(hk_ctx* ctx, void* stream);
  * material and the shading / NEE / shadow / temporal tail runs in that order.  Same results. */
 int hk_set_wavefront(hk_ctx* ctx, int enable);
 /* copy band-local rows [row0, row0+rows) of an output plane (e.g. the band's core rows for the
- * multi-GPU all-gather); dst is host (to_host=1) or device memory */
+ * multi-GPU all-gather); dst is host (to_host=1) or device memory.  On a stream other than the one
+ * the frame sequence runs on (e.g. a communication stream), the copy waits only for the work that
+ * produced the plane, device-side, and the context's next write of that plane waits for the copy: the
+ * frame stream itself never waits for the copy or for what follows it on `stream`. */
 int hk_copy_output_rows(hk_ctx* ctx, int output_id, uint32_t row0, uint32_t rows, void* dst, int to_host,
                         void* stream);
 /* copy reservoir buffer `id` (0..9) in the reference's AoS PackedReservoir layout */

@@ -168,7 +168,7 @@ class Oracle:
         C.memmove(p, data.ctypes.data, data.nbytes)
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 3)()
+        v = (C.c_uint64 * 4)()  # hk_counters (include/hikari_amd.h): the oracle traces every frame, [3] = 0
         self._L.hko_counters(self.ctx, v)
         return {"traverse_top": v[0], "traverse_emitter": v[1], "primary": v[2]}
 

@@ -18,3 +18,13 @@ def pytest_configure(config):
 def oracle_lib():
     import oracle
     return oracle.lib()
+
+
+@pytest.fixture
+def hk_options(monkeypatch):
+    """Runtime options (hk_set_option) for every HikariRenderer the test creates: a dict the test fills
+    before creating its contexts (kernel variants and schedules; results must not depend on them)."""
+    from hikari_amd import HikariRenderer
+    opts = {}
+    monkeypatch.setattr(HikariRenderer, "defaults", opts)
+    return opts

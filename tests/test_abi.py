@@ -37,7 +37,7 @@ def test_abi_version_and_defaults():
 
     import hikari_amd
     L = hikari_amd._abi.lib()
-    assert L.hk_abi_version() == 2
+    assert L.hk_abi_version() == 3
     s = hikari_amd._abi.hk_settings()
     L.hk_settings_default(C.byref(s))
     # HikariSettings::default() (lib.rs:435-455)
@@ -106,3 +106,22 @@ def test_struct_sizes_match_header(tmp_path):
         for f, _ in cls._fields_:
             assert int(out[f"{name}.{f}"]) == getattr(cls, f).offset, f"{name}.{f}"
     assert hikari_amd.RESERVOIR_DTYPE.itemsize == 64
+
+
+def test_runtime_options_documented():
+    """Every runtime option key (hk_option_name) is documented in include/hikari_amd.h's hk_set_option
+    comment, and nothing on the frame path reads the environment (options through the ABI)."""
+    import hikari_amd
+    L = hikari_amd._abi.lib()
+    keys, i = [], 0
+    while L.hk_option_name(i) is not None:
+        keys.append(L.hk_option_name(i).decode())
+        i += 1
+    assert len(keys) >= 15 and L.hk_option_name(-1) is None
+    root = Path(__file__).resolve().parents[1]
+    header = (root / "include" / "hikari_amd.h").read_text()
+    doc = header[header.index("Runtime options"):header.index("int hk_set_option")]
+    for k in keys:
+        assert re.search(r"\b" + k + r"\b", doc), f"option {k} not documented"
+    for src in (root / "bevy-hikari_amd" / "csrc").glob("*"):
+        assert "getenv" not in src.read_text(), f"{src.name} reads the environment"

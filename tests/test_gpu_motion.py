@@ -287,22 +287,22 @@ def test_host_gbuffer_planes_bit_exact():
 
 
 @pytest.mark.parametrize("lds", ["0", "1"])
-def test_forced_kernel_variants_bit_exact(monkeypatch, lds):
+def test_forced_kernel_variants_bit_exact(hk_options, lds):
     """Kernel variants the size thresholds normally pick only at large sizes, forced on a small
-    frame: k_direct_lit_w4 (4 waves per SIMD; HK_DIRECT_W4_MIN_PX=0 with HK_NO_FUSE), the fused
-    direct+emissive launch next to the indirect side stream (HK_FUSE_MIN_PX=0, HK_MERGE=0) and the
-    merged direct+indirect launch (k_light_merged, HK_MERGE=1: the default only for small frames without
+    frame: k_direct_lit_w4 (4 waves per SIMD; direct_w4_min_px=0 with fuse=0), the fused
+    direct+emissive launch next to the indirect side stream (fuse_min_px=0, merge=0) and the
+    merged direct+indirect launch (k_light_merged, merge=1: the default only for small frames without
     spatial reuse; here with spatial reuse after it) and the persistent-wave indirect pass
-    (k_indirect_persist, HK_PERSIST=1, an opt-in), each with and without LDS scene staging."""
+    (k_indirect_persist, persistent_indirect=1, an opt-in), each with and without LDS scene staging."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
-    monkeypatch.setenv("HK_LDS_SCENE", lds)
+    hk_options["lds_scene"] = int(lds)
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
     s = st.to_c()
-    for env in ({"HK_DIRECT_W4_MIN_PX": "0", "HK_NO_FUSE": "1"}, {"HK_FUSE_MIN_PX": "0", "HK_MERGE": "0"},
-                {"HK_MERGE": "1"}, {"HK_PERSIST": "1", "HK_MERGE": "0"}):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    for env in ({"direct_w4_min_px": 0, "fuse": 0}, {"fuse_min_px": 0, "merge": 0},
+                {"merge": 1}, {"persistent_indirect": 1, "merge": 0}):
+        hk_options.clear()
+        hk_options.update(lds_scene=int(lds), **env)
         scene, cam, lights, r, o = _pair("cornell", w, h, st, threads=0)
         errors = []
         for f in range(6):
@@ -317,12 +317,10 @@ def test_forced_kernel_variants_bit_exact(monkeypatch, lds):
                 break
         assert not errors, f"{env}: " + "\n".join(errors[:20])
         assert r.counters() == o.counters()
-        for k in env:
-            monkeypatch.delenv(k)
 
 
 @pytest.mark.parametrize("launch", ["fused", "separate"])
-def test_background_elision_bit_exact(monkeypatch, launch):
+def test_background_elision_bit_exact(hk_options, launch):
     """Background store elision (ChannelArgs::bg, hk_kernels.hip bg_elide): the direct / emissive
     launches (fused, or separate sharing one mask) and the indirect pass skip a background pixel's constant zero stores once
     every target buffer holds them.  A sequence that exercises every way the mask can go stale:
@@ -332,10 +330,10 @@ def test_background_elision_bit_exact(monkeypatch, launch):
     reservoir buffers bit-exact against the oracle (which never elides) on every frame."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     if launch == "fused":
-        monkeypatch.setenv("HK_FUSE_MIN_PX", "0")
+        hk_options["fuse_min_px"] = 0
     else:  # direct_lit and the emissive pass as two launches sharing the mask (k_direct_lit_w4 too)
-        monkeypatch.setenv("HK_NO_FUSE", "1")
-        monkeypatch.setenv("HK_DIRECT_W4_MIN_PX", "0")
+        hk_options["fuse"] = 0
+        hk_options["direct_w4_min_px"] = 0
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=False, denoise=True)
     scene, cam, lights, r, o = _pair("cornell", w, h, st)
@@ -380,7 +378,7 @@ def test_background_elision_bit_exact(monkeypatch, launch):
 
 
 @pytest.mark.parametrize("jitter", [0, 1], ids=["static", "taa_jitter"])
-def test_background_elision_spatial_pairs_bit_exact(monkeypatch, jitter):
+def test_background_elision_spatial_pairs_bit_exact(hk_options, jitter):
     """Background store elision with both spatial reuse passes on (emissive_spatial_reuse and
     indirect_spatial_reuse): the fused launch's background pixels then skip their own targets but
     still store the spatial pair (the spatial passes rewrite it with a repacked record), and with TAA
@@ -389,7 +387,7 @@ def test_background_elision_spatial_pairs_bit_exact(monkeypatch, jitter):
     bit-exact on every frame, including after garbage is uploaded over the spatial pairs."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     from hikari_amd.plugin import RESERVOIR_DTYPE
-    monkeypatch.setenv("HK_FUSE_MIN_PX", "0")
+    hk_options["fuse_min_px"] = 0
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, emissive_spatial_reuse=True, indirect_spatial_reuse=True,
                         denoise=True)

@@ -45,9 +45,9 @@ def _compare_frame(r, o, frame, errors):
 
 
 @pytest.fixture(params=["1", "0", "2"], ids=["lds_default", "lds_off", "lds_all"])
-def lds_mode(request, monkeypatch):
-    """HK_LDS_SCENE: scene arrays staged in LDS by the default kernels / none / every traversal kernel."""
-    monkeypatch.setenv("HK_LDS_SCENE", request.param)
+def lds_mode(request, hk_options):
+    """Option lds_scene: scene arrays staged in LDS by the default kernels / none / every traversal kernel."""
+    hk_options["lds_scene"] = int(request.param)
     return request.param
 
 
@@ -135,13 +135,13 @@ def test_full_size_bench_workloads_bit_exact(config, frames):
 
 
 @pytest.mark.parametrize("denoise", [True, False], ids=["denoise", "tone_only"])
-def test_frame_pipelining_bit_exact(monkeypatch, denoise):
-    """Frame pipelining forced on a small frame (HK_PIPELINE_MIN_PX=0): the G-buffer of frame f on
+def test_frame_pipelining_bit_exact(hk_options, denoise):
+    """Frame pipelining forced on a small frame (option pipeline_min_px=0): the G-buffer of frame f on
     its own stream next to frame f-1's light passes, frame f's tail (denoise, tone-sum) next to
     frame f+1's; every plane, reservoir and counter of every frame as the oracle's serial run,
     with readbacks after each frame and without (outputs compared after the last frame only)."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
-    monkeypatch.setenv("HK_PIPELINE_MIN_PX", "0")
+    hk_options["pipeline_min_px"] = 0
     w, h = 96, 72
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=denoise)
     scene, cam, lights, r, o = _setup(w, h, st)
@@ -163,7 +163,7 @@ def test_frame_pipelining_bit_exact(monkeypatch, denoise):
     assert r.counters() == o.counters()
 
 
-def test_device_pointer_after_sync_is_current(monkeypatch):
+def test_device_pointer_after_sync_is_current(hk_options):
     """The zero-copy route of INTEGRATION.md §3: with frame pipelining forced on, a reader that takes
     hk_output_device_ptr and makes its own stream wait with hk_sync reads the frame's finished
     planes (tone-mapped, denoised, G-buffer) — copied with hipMemcpyAsync on that stream, bit-equal
@@ -171,7 +171,7 @@ def test_device_pointer_after_sync_is_current(monkeypatch):
     import ctypes
 
     from hikari_amd import HikariSettings, Upscale, frame_inputs
-    monkeypatch.setenv("HK_PIPELINE_MIN_PX", "0")
+    hk_options["pipeline_min_px"] = 0
     # the HIP runtime libhikari_amd.so itself uses (torch may bring a second copy into the process)
     maps = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln]
     path = next((m for m in maps if m.startswith("/opt/rocm")), maps[0] if maps else "libamdhip64.so")
@@ -206,12 +206,11 @@ def test_device_pointer_after_sync_is_current(monkeypatch):
     hip.hipStreamDestroy(stream)
 
 
-def test_fallback_paths_bit_exact(monkeypatch):
+def test_fallback_paths_bit_exact(hk_options):
     """The paths the defaults switch off stay exact: one stream (no channel fork), walk nodes
     without leaf collapse, the G-buffer stack with its scratch overflow levels."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
-    for k, v in (("HK_CHANNEL_STREAMS", "0"), ("HK_NO_COLLAPSE", "1"), ("HK_GB_DEEP", "1")):
-        monkeypatch.setenv(k, v)
+    hk_options.update(channel_streams=0, leaf_collapse=0, gbuffer_deep=1)
     w, h = 64, 48
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
     scene, cam, lights, r, o = _setup(w, h, st)
@@ -643,14 +642,14 @@ def test_gpu_instance_update_matches_host_rebuild(scene_fn):
 
 @pytest.mark.parametrize("ratio_setting,taa,pipelined", [("SMAA_TU_2_0", "Jasmine", False), ("SMAA_TU_1_0", "Jasmine", False),
                                                          ("SMAA_TU_2_0", "None_", False), ("SMAA_TU_1_0", "Jasmine", True)])
-def test_post_process_smaa_taa_bit_exact(ratio_setting, taa, pipelined, monkeypatch):
+def test_post_process_smaa_taa_bit_exact(ratio_setting, taa, pipelined, hk_options):
     """SMAA TU4x + TAA Jasmine (hk_post_process) on the GPU vs the oracle, bit for bit, over
     frames with both jitter parities (the reference default pipeline is SMAA_TU_2_0 + Jasmine).
     `pipelined`: frame pipelining forced on (the post-process reads the previous G-buffer slot,
     which the next frame's G-buffer overwrites)."""
     from hikari_amd import HikariSettings, Taa, Upscale, _abi, frame_inputs
     if pipelined:
-        monkeypatch.setenv("HK_PIPELINE_MIN_PX", "0")
+        hk_options["pipeline_min_px"] = 0
     w, h = 62, 41
     st = HikariSettings(upscale=getattr(Upscale, ratio_setting), taa=getattr(Taa, taa))
     scene, cam, lights, r, o = _setup(w, h, st)
@@ -670,14 +669,14 @@ def test_post_process_smaa_taa_bit_exact(ratio_setting, taa, pipelined, monkeypa
 
 
 @pytest.mark.parametrize("mode", ["no_view", "no_temporal_reuse"])
-def test_spatial_reuse_without_view_planes_bit_exact(monkeypatch, mode):
+def test_spatial_reuse_without_view_planes_bit_exact(hk_options, mode):
     """Spatial reuse gathering the neighbours' own reservoir planes instead of the spatial view planes
-    (hk_device.h store_res_view): forced with HK_NO_SP_VIEW=1, and taken by the runtime when the temporal
+    (hk_device.h store_res_view): forced with spatial_view_planes=0, and taken by the runtime when the temporal
     pass does not store its records (temporal_reuse = false: the records in `cur` are older than any view
     plane).  Every plane and reservoir bit-exact against the oracle over 6 frames."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     if mode == "no_view":
-        monkeypatch.setenv("HK_NO_SP_VIEW", "1")
+        hk_options["spatial_view_planes"] = 0
     w, h = 64, 64
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, temporal_reuse=mode != "no_temporal_reuse")
     scene, cam, lights, r, o = _setup(w, h, st)

@@ -56,9 +56,9 @@ def _frames(scene_fn, w, h, settings, frames):
 
 @pytest.mark.parametrize("lds", ["0", "1"])
 @pytest.mark.parametrize("size", [(64, 64), (96, 72)])
-def test_wavefront_cornell_bit_exact(monkeypatch, lds, size):
+def test_wavefront_cornell_bit_exact(hk_options, lds, size):
     from hikari_amd import HikariSettings, Upscale
-    monkeypatch.setenv("HK_LDS_SCENE", lds)
+    hk_options["lds_scene"] = int(lds)
     _frames("cornell", size[0], size[1], HikariSettings(upscale=Upscale.SMAA_TU_1_0), 7)
 
 
@@ -80,9 +80,10 @@ def test_city_4k_16spp_bit_exact():
     """BASELINE configs[4] at full size: city.rs 3840x2160, 16 integrator sub-frames per displayed
     frame (each one reference frame: G-buffer, light passes with the wavefront indirect pass, spatial
     reuse, denoise, tone-sum), accumulated and resolved on the GPU, over 2 displayed frames.
-    * whole frame: the wavefront context equals a megakernel context (whose full-size parity with the
-      oracle test_full_size_bench_workloads_bit_exact establishes) on OUT_ACCUMULATED of both
-      displayed frames, every plane and reservoir buffer of the last sub-frame and the ray counters;
+    * whole frame: the wavefront context (G-buffer reuse on: 30 of the 32 sub-frames keep the planes they
+      find) equals a megakernel context tracing every sub-frame (whose full-size parity with the oracle
+      test_full_size_bench_workloads_bit_exact establishes) on OUT_ACCUMULATED of both displayed frames,
+      every plane and reservoir buffer of the last sub-frame and the ray counters;
     * against the oracle: rows 1040..1119 (through the sphere and the houses) rendered by the oracle
       as a band with a 40-row halo (exact for the band's own rows, test_gpu_row_bands_match_whole_frame),
       its 32 tone-mapped sub-frames accumulated in numpy (f32 running sum, / 16, rounded to f16),
@@ -99,7 +100,9 @@ def test_city_4k_16spp_bit_exact():
     desc = scene.build()
     ctx = []
     for wavefront in (True, False):
-        r = HikariRenderer(0)
+        # the wavefront context reuses the G-buffer of the static sub-frames (the default), the megakernel
+        # context traces every sub-frame (gbuffer_reuse = 0): their equality pins the reuse at full size
+        r = HikariRenderer(0, options={"gbuffer_reuse": 1 if wavefront else 0})
         r.set_noise()
         r.upload_scene(scene)
         r.resize(w, h, 1.0)
@@ -146,3 +149,4 @@ def test_city_4k_16spp_bit_exact():
             errors.append(m)
     assert not errors, "\n".join(errors[:20])
     assert ctx[0].counters() == ctx[1].counters()
+    assert ctx[0].primary_reused() == (2 * spp - 2) * w * h and ctx[1].primary_reused() == 0

@@ -15,7 +15,7 @@ timeout -k 10 300 python bench.py > $OUT/bench_default.json 2> $OUT/bench_defaul
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
    -d $R/$OUT/stats -o run -- python $R/bench.py --steps 20 --warmup 3 --cpu-budget 0 > $R/$OUT/stats.log 2>&1)
 # the same with every kernel alone (channel fork and frame pipelining off): the isolated durations of the roofline
-(cd /tmp && export TMPDIR=/tmp && HK_CHANNEL_STREAMS=0 HK_GB_PIPELINE=0 HK_DN_PIPELINE=0 timeout -k 10 300 rocprofv3 \
+(cd /tmp && export TMPDIR=/tmp && HK_BENCH_OPTS=channel_streams=0,gbuffer_pipeline=0,tail_pipeline=0 timeout -k 10 300 rocprofv3 \
    --kernel-trace --stats --output-format csv -d $R/$OUT/stats_isolated -o run -- python $R/bench.py --steps 20 --warmup 3 \
    --cpu-budget 0 > $R/$OUT/stats_isolated.log 2>&1)
 # the RCCL path itself at world size 1 (communicator, per-frame all-gather, reductions) on the one GPU

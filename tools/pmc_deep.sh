@@ -6,7 +6,7 @@ OUT=$1; CFG=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/$OUT
 cd /tmp && export TMPDIR=/tmp
-export HK_CHANNEL_STREAMS=0 HK_GB_PIPELINE=0 HK_DN_PIPELINE=0
+export HK_BENCH_OPTS=channel_streams=0,gbuffer_pipeline=0,tail_pipeline=0
 i=0
 for group in \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE" \

@@ -8,7 +8,7 @@ OUT=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/$OUT
 cd /tmp && export TMPDIR=/tmp
-export HK_CHANNEL_STREAMS=0 HK_GB_PIPELINE=0 HK_DN_PIPELINE=0
+export HK_BENCH_OPTS=channel_streams=0,gbuffer_pipeline=0,tail_pipeline=0
 for cfg in "$@"; do
   for group in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $group --output-format csv -d $R/$OUT/$cfg/$group -o run -- \
