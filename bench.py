@@ -39,7 +39,8 @@ import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Taa, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import band_of, halo_rows, stripe_gather_rows, use_stripes  # noqa: E402
+from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, halo_rows, rebalance,  # noqa: E402
+                              stripe_gather_rows, use_stripes)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -278,7 +279,10 @@ def main():
     # defaults are the tuned configuration
     bench_opts = {kv.split("=")[0]: float(kv.split("=")[1])
                   for kv in os.environ.get("HK_BENCH_OPTS", "").replace("+", ",").split(",") if kv}
-    r.set_options(bench_opts)
+    # G-buffer reuse (skipping the primary-ray trace when the slot already holds the frame's planes) only
+    # for the sub-frames of an accumulated frame (configs[4]); a 1-spp frame traces its G-buffer every time,
+    # as the reference rasterises its prepass every frame, even with the static camera of the bench
+    r.set_options({"gbuffer_reuse": 1 if cfg.get("spp", 1) > 1 else 0, **bench_opts})
     r.set_noise()
     r.upload_scene(scene)
     r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
@@ -286,17 +290,47 @@ def main():
     # overrides the config (0 = megakernel, 1 = wavefront) for comparisons
     wavefront = os.environ.get("HK_BENCH_WAVEFRONT", "1" if cfg.get("wavefront") else "0") == "1"
     r.set_wavefront(wavefront)
+    bounds, balance = None, []
     if stripes:
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
     elif dist_on:
-        b = band_of(rank, world, H)
-        band = b.rows
+        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 2) of a short
+        # calibration on the current bands — frames 0..5 rendered, 3..5 timed per rank, the times all-gathered
+        # — each moving the boundaries to equal measured cost.  Then every rank starts the run from frame 0
+        # on its final band (hk_resize zero-fills the reservoirs, as at the start of any run).
+        bounds = equal_bounds(world, H)
+        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "2")) if world > 1 else 0):
+            b = band_of(rank, world, H, bounds)
+            r.resize(W, H, 1.0, b.y0, b.rows)
+            for f in range(6):
+                if f == 3:
+                    torch.cuda.synchronize()
+                    t_cal = time.perf_counter()
+                fi = frame_inputs(f, cam, lights, W, H)
+                r.render_gbuffer(fi)
+                r.render_frame(s, fi)
+                if st.denoise:
+                    r.denoise(s, fi)
+                r.tone_sum(s)
+            r.sync()
+            torch.cuda.synchronize()
+            t_cal = torch.tensor([(time.perf_counter() - t_cal) / 3.0], dtype=torch.float64,
+                                 device="cpu" if rehearsal else "cuda")
+            times = torch.zeros(world, dtype=torch.float64, device=t_cal.device)
+            dist.all_gather_into_tensor(times, t_cal)
+            times = times.cpu().numpy()
+            balance.append({"bounds": list(bounds), "ms": [round(float(t) * 1e3, 4) for t in times]})
+            bounds = rebalance(bounds, times)
+        b = band_of(rank, world, H, bounds)
         r.resize(W, H, 1.0, b.y0, b.rows)
+        band, gather_index = band_gather_rows(bounds)
     else:
         band = H
         r.resize(W, H, 1.0)
     row0, rows, core0, core_rows = r.band_info()
+    # the gathered rows back in frame order (stripes; uneven bands) on a side stream after each gather
+    reorder = stripes or (bounds is not None and list(bounds) != equal_bounds(world, H))
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
@@ -310,7 +344,7 @@ def main():
     full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
         if dist_on else None
     pending = [None, None]
-    if stripes:  # stripes back in frame order, on a side stream after each gather
+    if reorder:  # stripes / uneven bands back in frame order, on a side stream after each gather
         frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
         index_t = torch.from_numpy(gather_index).to("cuda")
         side = torch.cuda.Stream()
@@ -361,7 +395,7 @@ def main():
             with torch.cuda.stream(comm):
                 if pending[k] is not None:
                     pending[k].wait()  # device-side: the comm stream waits for that gather
-                if stripes and reorder_done[k] is not None:
+                if reorder and reorder_done[k] is not None:
                     comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
                 r.copy_output_rows(shown, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
                 if rehearsal:
@@ -370,7 +404,7 @@ def main():
                     full_t[k].copy_(torch.cat(parts))
                 else:
                     pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
-            if stripes:
+            if reorder:
                 with torch.cuda.stream(side):
                     if pending[k] is not None:
                         pending[k].wait()
@@ -385,7 +419,7 @@ def main():
                 pending[k].wait()
                 pending[k] = None
         torch.cuda.current_stream().wait_stream(comm)
-        if stripes:
+        if reorder:
             torch.cuda.current_stream().wait_stream(side)
 
     for f in range(args.warmup):
@@ -511,7 +545,9 @@ def main():
                        "rays_per_frame": int(rays // (args.steps * spp)),
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
-                                       f"row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU"},
+                                       f"cost-balanced row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU",
+                       "band_bounds": None if bounds is None else [int(v) for v in bounds],
+                       "band_calibration": balance or None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "hbm_frac": None if traffic is None else

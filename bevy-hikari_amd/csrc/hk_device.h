@@ -1158,11 +1158,27 @@ HKD void normal_basis(f3 n, f3& t, f3& b)
 HKD f3 basis_mul(f3 t, f3 b, f3 n, f3 d) { return (t * d.x + b * d.y) + n * d.z; }
 HKD f3 emissive_radiance(f4 e) { return xyz(e) * (255.0f * e.w); }
 
+// select_light_candidate (light.wgsl:599-708) in two halves around its emitter BLAS walk, so that a kernel
+// can run the walks of a whole workgroup as one compacted batch between them (k_direct_fused_w4's CW
+// variant): light_pick_begin runs everything before the walk (directional cone sample, light-BVH reservoir
+// pick, alias-table triangle sample, the ray towards the sampled point in world and emitter-local space),
+// light_pick_end everything after it.  select_light_candidate = begin, the walk, end: the same statements
+// in the same order.
+struct LightPick {
+    LightCandidate cand;
+    f3 rand_direction;
+    Ray ray;    // world: biased origin, direction towards the sampled point (inv_direction unused)
+    Ray local;  // the emitter instance's local ray of the walk
+    uint32_t picked;  // emissive record of the pick
+    float count;
+    bool emitter;     // an emitter was picked (light_pick_end must run)
+    bool walk;        // ... and the walk runs (the sampled direction faces the normal)
+};
 template <bool COUNT>
-HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 rand, f3 position, f3 normal,
-                                          uint32_t instance, HitInfo& info, uint32_t& n_emitter)
+HKD void light_pick_begin(const Scene& sc, const Frame& F, f4 rand, f3 position, f3 normal, uint32_t instance,
+                          HitInfo& info, uint32_t& n_emitter, LightPick& L)
 {
-    LightCandidate candidate;
+    LightCandidate& candidate = L.cand;
     candidate.max_distance = HK_F32_MAX;
     candidate.min_distance = DISTANCE_MAX;
     candidate.emissive_instance = DONT_SAMPLE_EMISSIVE;
@@ -1170,10 +1186,12 @@ HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 ra
     f3 bt, bb;
     normal_basis(cone, bt, bb);
     f3 rand_direction = basis_mul(bt, bb, cone, xyz(sample_uniform_cone(mk2(rand.z, rand.w), F.cos_solar_angle)));
+    L.rand_direction = rand_direction;
     candidate.direction = rand_direction;
     candidate.p = 1.0f;
     info = empty_hit_info(position, rand_direction);
-    if (instance == DONT_SAMPLE_EMISSIVE) return candidate;
+    L.emitter = L.walk = false;
+    if (instance == DONT_SAMPLE_EMISSIVE) return;
 
     uint32_t picked = 0u;
     float count = 0.0f;
@@ -1206,7 +1224,10 @@ HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 ra
             index = inside ? entry : exit;
         }
     }
+    L.picked = picked;
+    L.count = count;
     if (candidate.emissive_instance != DONT_SAMPLE_EMISSIVE) {
+        L.emitter = true;
         const hk_emissive& emissive = sc.emissives[picked];
         uint32_t len = emissive.alias_table[1];
         uint32_t alias_index = f2u32(rand.x * (float)len);
@@ -1220,41 +1241,65 @@ HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 ra
         f2 b = mk2(1.0f - srx, rand.w * srx);
         f3 p = local_to_world_point(ein, (v0 * b.x + v1 * b.y) + v2 * ((1.0f - b.x) - b.y));
 
-        Hit hit;
-        hit.uv = mk2(0, 0);
-        hit.distance = HK_F32_MAX;
-        hit.instance_index = HK_U32_MAX;
-        hit.primitive_index = HK_U32_MAX;
-        Ray ray;
+        Ray& ray = L.ray;
         ray.origin = position + normal * RAY_BIAS;
         ray.direction = normalize(p - position);
         ray.inv_direction = mk3(0, 0, 0);
-        Ray r;
+        Ray& r = L.local;
         r.origin = world_to_local_point(ein, ray.origin);
         r.direction = world_to_local_dir(ein, ray.direction);
         r.inv_direction = inv(r.direction);
         candidate.direction = ray.direction;
-        bool traced = false;
         if (dot(candidate.direction, normal) > 0.0f) {
             if (COUNT) n_emitter++;
-            traced = traverse_bottom(sc, hit, r, ein.mesh.node[0], ein.mesh.node[1], ein.mesh.primitive, 0.0f);
-        }
-        if (traced) {
-            hit.instance_index = emissive.instance;
-            info = hit_info(sc, ray, hit);
-            candidate.max_distance = hit.distance;
-            candidate.min_distance = hit.distance - 0.1f;
-            f3 delta = xyz(info.position) - position;
-            candidate.p = dot(delta, delta) / fabsf(dot(ray.direction, info.normal) * emissive.surface_area);
-            candidate.p = candidate.p / count;
-        } else {
-            info = empty_hit_info(ray.origin, ray.direction);
-            candidate.emissive_instance = DONT_SAMPLE_EMISSIVE;
-            candidate.direction = rand_direction;
-            candidate.p = 1.0f;
+            L.walk = true;
         }
     }
-    return candidate;
+}
+// the walk of L (traverse_bottom over the picked emitter's BLAS, closest hit): hit starts empty
+HKD bool light_pick_walk(const Scene& sc, const LightPick& L, Hit& hit)
+{
+    hit.uv = mk2(0, 0);
+    hit.distance = HK_F32_MAX;
+    hit.instance_index = HK_U32_MAX;
+    hit.primitive_index = HK_U32_MAX;
+    if (!L.walk) return false;
+    const hk_instance& ein = get_instance(sc, L.cand.emissive_instance);
+    return traverse_bottom(sc, hit, L.local, ein.mesh.node[0], ein.mesh.node[1], ein.mesh.primitive, 0.0f);
+}
+// after the walk (traced: it ran and hit; hit: its result); only when L.emitter
+HKD void light_pick_end(const Scene& sc, LightPick& L, f3 position, Hit hit, bool traced, HitInfo& info)
+{
+    LightCandidate& candidate = L.cand;
+    const hk_emissive& emissive = sc.emissives[L.picked];
+    const Ray& ray = L.ray;
+    if (traced) {
+        hit.instance_index = emissive.instance;
+        info = hit_info(sc, ray, hit);
+        candidate.max_distance = hit.distance;
+        candidate.min_distance = hit.distance - 0.1f;
+        f3 delta = xyz(info.position) - position;
+        candidate.p = dot(delta, delta) / fabsf(dot(ray.direction, info.normal) * emissive.surface_area);
+        candidate.p = candidate.p / L.count;
+    } else {
+        info = empty_hit_info(ray.origin, ray.direction);
+        candidate.emissive_instance = DONT_SAMPLE_EMISSIVE;
+        candidate.direction = L.rand_direction;
+        candidate.p = 1.0f;
+    }
+}
+template <bool COUNT>
+HKD LightCandidate select_light_candidate(const Scene& sc, const Frame& F, f4 rand, f3 position, f3 normal,
+                                          uint32_t instance, HitInfo& info, uint32_t& n_emitter)
+{
+    LightPick L;
+    light_pick_begin<COUNT>(sc, F, rand, position, normal, instance, info, n_emitter, L);
+    if (L.emitter) {
+        Hit hit;
+        const bool traced = light_pick_walk(sc, L, hit);
+        light_pick_end(sc, L, position, hit, traced, info);
+    }
+    return L.cand;
 }
 
 // ------------------------------------------------------------------ shading (light.wgsl:714-908 + Bevy PBR)

@@ -404,19 +404,33 @@ HKD float* park_area()
     return park;
 }
 
-// PARK: 0 = the validation block keeps the reservoir in registers, 1 = parks it in a static LDS array,
-// 2 = in the launch's dynamic LDS (k_light_merged: the direct and indirect workgroups share one buffer)
-template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, int PARK = 0>
-HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel P, uint32_t& n_top,
-                     uint32_t& n_emitter, Surface* surface_out = nullptr, const Surface* surface_in = nullptr)
+// direct_lit (light.wgsl:1044-1261) in three parts, so that a kernel can run the candidate block's emitter
+// walk for a whole workgroup at once between them (k_direct_fused_w4's CW variant): direct_begin runs the
+// pass up to that walk (or the whole background pixel), direct_candidate the rest of the candidate block
+// from the walk's result, direct_finish the validation block and the stores.  direct_body = the three with
+// the walk in between: the same statements in the same order.
+struct DirectState {
+    Sample s;
+    Reservoir r;
+    HitInfo info;
+    Ray ray;
+    LightPick L;
+    f4 position;
+    f2 previous_uv;
+    bool cand_block;  // the candidate block runs (light.wgsl:1096-1107)
+};
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE>
+HKD bool direct_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel& P, DirectState& D,
+                      uint32_t& n_emitter)
 {
     const Frame& F = A.F;
     const int32_t idx = P.idx;
     const f2 uv = P.uv;
     f4 pd = P.pd;
-    f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
+    D.position = mk4(pd.x, pd.y, pd.z, 1.0f);
     float depth = pd.w;
-    Sample s = zero_sample();
+    Sample& s = D.s;
+    s = zero_sample();
     if (depth < HK_F32_EPSILON) {
         Reservoir r = zero_reservoir();
         set_reservoir(r, s, 0.0f);
@@ -431,53 +445,87 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
         }
         C.variance[idx] = 0.0f;
         store_rgba16f(C.render, idx, mk4(0, 0, 0, 0));
-        return;
+        D.cand_block = false;
+        return false;
     }
     f3 normal = P.normal;
-    uint32_t im_x = f2u32(P.imf.x), im_y = f2u32(P.imf.y);
+    uint32_t im_x = f2u32(P.imf.x);
     f4 velocity_uv = P.velocity_uv;
 
     s.random = P.random;
-    s.visible_position = mk4(position.x, position.y, position.z, depth);
+    s.visible_position = mk4(D.position.x, D.position.y, D.position.z, depth);
     s.visible_normal = normal;
     s.visible_instance = im_x;
 
-    Ray ray;
-    ray.origin = ray.direction = ray.inv_direction = mk3(0, 0, 0);
-    HitInfo info = empty_hit_info(mk3(0, 0, 0), mk3(0, 0, 0));
+    D.ray.origin = D.ray.direction = D.ray.inv_direction = mk3(0, 0, 0);
+    D.info = empty_hit_info(mk3(0, 0, 0), mk3(0, 0, 0));
 
     f2 juv = jittered_uv(F, uv, 0.25f);
-    f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
-    Reservoir r = load_previous(F, C.prev, previous_uv);
-    if (!check_previous_reservoir(r, s) && uv_inside_closed(previous_uv)) {
-        int32_t px = f2i32(previous_uv.x * (float)F.s[0]);
-        int32_t py = f2i32(previous_uv.y * (float)F.s[1]);
+    D.previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
+    Reservoir& r = D.r;
+    r = load_previous(F, C.prev, D.previous_uv);
+    if (!check_previous_reservoir(r, s) && uv_inside_closed(D.previous_uv)) {
+        int32_t px = f2i32(D.previous_uv.x * (float)F.s[0]);
+        int32_t py = f2i32(D.previous_uv.y * (float)F.s[1]);
         store_res(C.prev_spatial, s_index(F, px, py), r);
     }
 
     const uint32_t validate_interval = EMISSIVE_LIT ? F.emissive_validate_interval : F.direct_validate_interval;
     const uint32_t select_light_instance = EMISSIVE_LIT ? im_x : DONT_SAMPLE_EMISSIVE;
-
-    if (!VALIDATE || umod(F.number, validate_interval) != 0u || r.count < 4.0f) {
-        LightCandidate cand = select_light_candidate<true>(sc, F, s.random, xyz(s.visible_position), s.visible_normal,
-                                                           select_light_instance, info, n_emitter);
-        ray.origin = xyz(position) + normal * RAY_BIAS;
-        ray.direction = cand.direction;
-        ray.inv_direction = inv(ray.direction);
-        bool trace = dot(cand.direction, normal) > 0.0f && cand.p > 0.0f;
-        if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
-        if (trace) {
-            n_top++;
-            Hit hit = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
-            occlude_hit_info(ray, hit, info);
-            s.radiance = EMISSIVE_LIT ? input_radiance(sc, F, ray, info, false, cand.emissive_instance, false)
-                                      : input_radiance(sc, F, ray, info, true, DONT_SAMPLE_EMISSIVE, false);
-        }
-        s.sample_position = info.position;
-        s.sample_normal = info.normal;
-        float w_new = cand.p > 0.0f ? lum(xyz(s.radiance)) / cand.p : 0.0f;
-        temporal_restir(r, s, w_new, F.max_temporal_reuse_count);
+    D.cand_block = !VALIDATE || umod(F.number, validate_interval) != 0u || r.count < 4.0f;
+    if (D.cand_block)
+        light_pick_begin<true>(sc, F, s.random, xyz(s.visible_position), s.visible_normal, select_light_instance, D.info,
+                               n_emitter, D.L);
+    return true;
+}
+// the candidate block after its emitter walk (hit, traced: light_pick_walk's result)
+template <bool EMISSIVE_LIT>
+HKD void direct_candidate(const FrameArgs& A, const Scene& sc, const DirectPixel& P, DirectState& D, const Hit& walk_hit,
+                          bool traced, uint32_t& n_top)
+{
+    const Frame& F = A.F;
+    Sample& s = D.s;
+    if (D.L.emitter) light_pick_end(sc, D.L, xyz(s.visible_position), walk_hit, traced, D.info);
+    const LightCandidate cand = D.L.cand;
+    const f3 normal = P.normal;
+    Ray& ray = D.ray;
+    ray.origin = xyz(D.position) + normal * RAY_BIAS;
+    ray.direction = cand.direction;
+    ray.inv_direction = inv(ray.direction);
+    bool trace = dot(cand.direction, normal) > 0.0f && cand.p > 0.0f;
+    if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
+    if (trace) {
+        n_top++;
+        Hit hit = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
+        occlude_hit_info(ray, hit, D.info);
+        s.radiance = EMISSIVE_LIT ? input_radiance(sc, F, ray, D.info, false, cand.emissive_instance, false)
+                                  : input_radiance(sc, F, ray, D.info, true, DONT_SAMPLE_EMISSIVE, false);
     }
+    s.sample_position = D.info.position;
+    s.sample_normal = D.info.normal;
+    float w_new = cand.p > 0.0f ? lum(xyz(s.radiance)) / cand.p : 0.0f;
+    temporal_restir(D.r, s, w_new, F.max_temporal_reuse_count);
+}
+
+// PARK: 0 = the validation block keeps the reservoir in registers, 1 = parks it in a static LDS array,
+// 2 = in the launch's dynamic LDS (k_light_merged: the direct and indirect workgroups share one buffer)
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, int PARK = 0>
+HKD void direct_finish(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel& P, DirectState& D,
+                       uint32_t& n_top, uint32_t& n_emitter, Surface* surface_out = nullptr,
+                       const Surface* surface_in = nullptr)
+{
+    const Frame& F = A.F;
+    const int32_t idx = P.idx;
+    const f4 position = D.position;
+    Sample& s = D.s;
+    Reservoir& r = D.r;
+    HitInfo& info = D.info;
+    Ray& ray = D.ray;
+    const f2 previous_uv = D.previous_uv;
+    const uint32_t im_x = f2u32(P.imf.x), im_y = f2u32(P.imf.y);
+    const f4 velocity_uv = P.velocity_uv;
+    const uint32_t validate_interval = EMISSIVE_LIT ? F.emissive_validate_interval : F.direct_validate_interval;
+    const uint32_t select_light_instance = EMISSIVE_LIT ? im_x : DONT_SAMPLE_EMISSIVE;
 
     if (VALIDATE && umod(F.number, validate_interval) == 0u) {
         float* lds = nullptr;
@@ -552,6 +600,22 @@ HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
     out = out * r.w;
     if (RENDER_EMISSIVE) out = out + emissive_radiance(surface.emissive);
     store_rgba16f(C.render, idx, mk4(out.x, out.y, out.z, 1.0f));
+}
+
+
+template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE = true, int PARK = 0>
+HKD void direct_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, const DirectPixel P, uint32_t& n_top,
+                     uint32_t& n_emitter, Surface* surface_out = nullptr, const Surface* surface_in = nullptr)
+{
+    DirectState D;
+    if (!direct_begin<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, P, D, n_emitter)) return;
+    if (D.cand_block) {
+        Hit hit;
+        bool traced = false;
+        if (D.L.emitter) traced = light_pick_walk(sc, D.L, hit);
+        direct_candidate<EMISSIVE_LIT>(A, sc, P, D, hit, traced, n_top);
+    }
+    direct_finish<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE, PARK>(A, sc, C, P, D, n_top, n_emitter, surface_out, surface_in);
 }
 
 // Background store elision (ChannelArgs::bg).  A background pixel (G-buffer depth 0, or every
@@ -710,6 +774,141 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             direct_body<false, true, VD, !LDS>(A, sc, C0, P, n_top, n_emitter, &surface);
             direct_body<true, false, VE, !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
         }
+    }
+    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    wave_count(A.cnt.top, n_top);
+    wave_count(A.cnt.emitter, n_emitter);
+}
+
+// Emitter walks of a workgroup as one compacted batch (the CW variant of the fused launch).  In city the
+// emissive pass picks an emitter for ~3 of 4 covered pixels: mostly the small lamp meshes (a 3-visit BLAS
+// walk) and for ~13 % the emissive sphere (13-180 visits).  A wave runs the walk until its longest lane
+// ends, so the one or two sphere walkers in most waves kept the whole wave in the walk: SIMD lane efficiency
+// 0.14 (tools/walk_lanes.py, oracle statistics of city frames).  Here the workgroup's walk requests are
+// written to LDS, queued long walks first (emitter BLAS with more than CW_LONG_NODES nodes) then short ones,
+// and thread t runs queue entry t: the long walks of the 4 waves share one or two waves (model: 0.35).  A
+// walk's result does not depend on the thread that runs it, so the results are those of the per-pixel walk.
+constexpr uint32_t CW_LONG_NODES = 16u;
+constexpr int CW_WORDS = 9;  // request: local origin 3, direction 3, BLAS node offset, node count, primitive offset
+HKD float* cw_area()
+{
+    __shared__ float cw[CW_WORDS * 256];
+    return cw;
+}
+// every thread of the workgroup calls this at the same point (barriers); need = the thread's pixel walks
+HKD bool compact_emitter_walks(const Scene& sc, float* lds, const LightPick& L, bool need, Hit& hit)
+{
+    __shared__ uint32_t queue[256];
+    __shared__ uint32_t wave_counts[8];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t node_offset = 0u, node_count = 0u;
+    if (need) {
+        const hk_instance& ein = get_instance(sc, L.cand.emissive_instance);
+        node_offset = ein.mesh.node[0];
+        node_count = ein.mesh.node[1];
+        lds[0 * 256 + t] = L.local.origin.x;
+        lds[1 * 256 + t] = L.local.origin.y;
+        lds[2 * 256 + t] = L.local.origin.z;
+        lds[3 * 256 + t] = L.local.direction.x;
+        lds[4 * 256 + t] = L.local.direction.y;
+        lds[5 * 256 + t] = L.local.direction.z;
+        lds[6 * 256 + t] = __uint_as_float(node_offset);
+        lds[7 * 256 + t] = __uint_as_float(node_count);
+        lds[8 * 256 + t] = __uint_as_float(ein.mesh.primitive);
+    }
+    const bool lng = need && node_count > CW_LONG_NODES;
+    const uint64_t m_long = __ballot(lng), m_short = __ballot(need && !lng);
+    if (lane == 0u) {
+        wave_counts[2u * w] = (uint32_t)__popcll(m_long);
+        wave_counts[2u * w + 1u] = (uint32_t)__popcll(m_short);
+    }
+    __syncthreads();
+    uint32_t n_long = 0u, n_short = 0u, below_long = 0u, below_short = 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+        const uint32_t a = wave_counts[2u * k], b = wave_counts[2u * k + 1u];
+        below_long += k < w ? a : 0u;
+        below_short += k < w ? b : 0u;
+        n_long += a;
+        n_short += b;
+    }
+    if (need) {
+        const uint64_t below = (1ull << lane) - 1ull;
+        const uint32_t pos = lng ? below_long + (uint32_t)__popcll(m_long & below)
+                                 : n_long + below_short + (uint32_t)__popcll(m_short & below);
+        queue[pos] = t;
+    }
+    __syncthreads();
+    if (t < n_long + n_short) {
+        const uint32_t o = queue[t];
+        Ray r;
+        r.origin = mk3(lds[0 * 256 + o], lds[1 * 256 + o], lds[2 * 256 + o]);
+        r.direction = mk3(lds[3 * 256 + o], lds[4 * 256 + o], lds[5 * 256 + o]);
+        r.inv_direction = inv(r.direction);
+        Hit h;
+        h.uv = mk2(0, 0);
+        h.distance = HK_F32_MAX;
+        h.instance_index = HK_U32_MAX;
+        h.primitive_index = HK_U32_MAX;
+        const bool traced = traverse_bottom(sc, h, r, __float_as_uint(lds[6 * 256 + o]), __float_as_uint(lds[7 * 256 + o]),
+                                            __float_as_uint(lds[8 * 256 + o]), 0.0f);
+        // the result over the request's own slots (read only by this thread)
+        lds[0 * 256 + o] = h.uv.x;
+        lds[1 * 256 + o] = h.uv.y;
+        lds[2 * 256 + o] = h.distance;
+        lds[3 * 256 + o] = __uint_as_float(h.primitive_index);
+        lds[4 * 256 + o] = traced ? 1.0f : 0.0f;
+    }
+    __syncthreads();
+    hit.uv = mk2(0, 0);
+    hit.distance = HK_F32_MAX;
+    hit.instance_index = HK_U32_MAX;
+    hit.primitive_index = HK_U32_MAX;
+    if (!need) return false;
+    hit.uv = mk2(lds[0 * 256 + t], lds[1 * 256 + t]);
+    hit.distance = lds[2 * 256 + t];
+    hit.primitive_index = __float_as_uint(lds[3 * 256 + t]);
+    return lds[4 * 256 + t] != 0.0f;
+}
+
+// k_direct_fused_w4 on the frames that validate neither pass's emitter picks (VE false) with the emissive
+// pass's emitter walks compacted per workgroup (compact_emitter_walks).  Every thread reaches the barriers:
+// the pixel's work is predicated, not returned from.  The walk requests live in the direct validation
+// block's park columns when that block runs (VD: a thread's own column, written after its own block ended)
+// or in their own LDS array.
+template <bool VD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_fused_cw(FrameArgs A, ChannelArgs C0,
+                                                                                                   ChannelArgs C1)
+{
+    const Scene& sc = A.sc;
+    float* lds = VD ? park_area() : cw_area();
+    int32_t x, y;
+    uint32_t n_top = 0, n_emitter = 0;
+    const bool on = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    DirectPixel P;
+    uint32_t bg = BG_SKIP_ALL;
+    if (on) {
+        P = load_direct_pixel(A, x, y);
+        bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
+        if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
+            const Reservoir z = background_reservoir();
+            store_res(C1.spatial, P.idx, z);
+            store_res(C1.prev_spatial, P.idx, z);
+        }
+    }
+    const bool work = on && bg == BG_STORE;
+    Surface surface;
+    DirectState D;
+    bool lit = false;
+    if (work) {
+        direct_body<false, true, VD, 1>(A, sc, C0, P, n_top, n_emitter, &surface);
+        lit = direct_begin<true, false, false>(A, sc, C1, P, D, n_emitter);
+    }
+    Hit hit;
+    const bool traced = compact_emitter_walks(sc, lds, D.L, lit && D.L.walk, hit);
+    if (lit) {
+        direct_candidate<true>(A, sc, P, D, hit, traced, n_top);
+        direct_finish<true, false, false, 0>(A, sc, C1, P, D, n_top, n_emitter, nullptr, &surface);
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -1794,7 +1993,10 @@ static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const Chan
                            uint32_t lds, hipStream_t st)
 {
     const bool w4 = A.opt.fused_w4 != 0;
-    if (!LDS && w4 && ve) {
+    if (!LDS && w4 && !ve && A.opt.compact_emitter) {
+        if (vd) hipLaunchKernelGGL((k_direct_fused_cw<true>), g, dim3(256), lds, st, A, C0, C1);
+        else hipLaunchKernelGGL((k_direct_fused_cw<false>), g, dim3(256), lds, st, A, C0, C1);
+    } else if (!LDS && w4 && ve) {
         if (vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
         else hipLaunchKernelGGL((k_direct_fused_w4<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
     } else if (vd && ve) hipLaunchKernelGGL((k_direct_fused<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);

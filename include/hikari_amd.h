@@ -215,6 +215,8 @@ void hk_settings_default(hk_settings* out);
  *   lds_scene (1)            0 no LDS scene staging, 1 where measured faster, 2 every traversal kernel
  *   gbuffer_stack_full (0), gbuffer_deep (0), direct_w4_min_px (4e5), fused_w4 (1),
  *   persistent_indirect (0)  kernel-variant choices (tests force each variant with them)
+ *   compact_emitter (1)      the fused direct/emissive launch runs a workgroup's emitter BLAS walks as one
+ *                            compacted batch (long walks first) on frames without emissive validation
  * hk_set_option returns HK_ERR_INVALID for an unknown key or a value outside the key's range. */
 int hk_set_option(hk_ctx* ctx, const char* key, double value);
 int hk_get_option(const hk_ctx* ctx, const char* key, double* value);

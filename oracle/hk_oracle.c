@@ -475,7 +475,15 @@ static __thread int hko_class = 3;
 static __thread unsigned hko_ray_steps; /* node visits + leaf tests of the current traverse_top */
 uint32_t* hko_steps_out;                 /* per-ray steps of hko_trace, if set */
 unsigned long long hko_hit_infos;        /* hit_info calls (3 vertices + instance + material fetched) */
-#define HKO_STAT(k) (__atomic_fetch_add(&hko_stats[hko_class][k], 1ull, __ATOMIC_RELAXED), hko_ray_steps++)
+/* per-pixel walk steps of the light passes, if set: [pass 0 direct_lit, 1 emissive, 2 indirect][class][s pixel],
+ * node visits + leaf tests of every walk of that class (the lane-efficiency model of tools/walk_lanes.py) */
+uint32_t* hko_pixel_steps_out;
+static __thread int32_t hko_pixel = -1, hko_pass = 0;
+static __thread uint32_t hko_npix;
+#define HKO_STAT(k) (__atomic_fetch_add(&hko_stats[hko_class][k], 1ull, __ATOMIC_RELAXED), hko_ray_steps++, \
+                     (hko_pixel_steps_out && hko_pixel >= 0 ?                                                  \
+                      (void)hko_pixel_steps_out[((size_t)hko_pass * 4u + (size_t)hko_class) * hko_npix + (size_t)hko_pixel]++ \
+                      : (void)0))
 #else
 #define HKO_STAT(k) ((void)0)
 #endif
@@ -2055,11 +2063,20 @@ static void run_pass(hko_ctx* c, const Pass* P, Kind kind)
         {
             if (!row_on(c, y)) continue;
             for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) {
+#ifdef HKO_STATS
+                hko_npix = c->s[0] * c->s[1];
+                hko_pixel = (int32_t)(x + (int32_t)c->s[0] * y);
+                hko_pass = kind == K_INDIRECT ? 2 : (P->emissive_lit ? 1 : 0);
+                if (kind == K_SPATIAL) hko_pixel = -1;
+#endif
                 if (kind == K_DIRECT) direct_lit(P, &k, x, y);
                 else if (kind == K_INDIRECT) indirect_lit_ambient(P, &k, x, y);
                 else spatial_reuse(P, x, y);
             }
         }
+#ifdef HKO_STATS
+        hko_pixel = -1;
+#endif
         add_counts(c, &k);
     }
 }

@@ -78,11 +78,19 @@ def test_cornell_frames_bit_exact(size, lds_mode):
     assert r.counters() == o.counters()
 
 
-@pytest.mark.parametrize("config,frames", [("cornell-1080p-nee", 4), ("scene-1080p-full", 2), ("city-4k", 2)])
-def test_full_size_bench_workloads_bit_exact(config, frames):
+# uneven 8-band split of city 3840x2160 (cost-balanced bands as bench.py's calibration produces them:
+# narrow bands over the houses and the sphere in the lower half)
+CITY_UNEVEN = [0, 464, 848, 1104, 1296, 1488, 1688, 1904, 2160]
+
+
+@pytest.mark.parametrize("config,frames,uneven", [("cornell-1080p-nee", 4, False), ("scene-1080p-full", 2, False),
+                                                  ("city-4k", 2, False), ("city-4k", 2, True)],
+                         ids=["cornell-1080p-nee-4", "scene-1080p-full-2", "city-4k-2", "city-4k-uneven-2"])
+def test_full_size_bench_workloads_bit_exact(config, frames, uneven):
     """The bench workloads themselves (BASELINE configs 2-4 at 1920x1080 and 3840x2160): every output plane
     of every frame, all reservoir buffers of the last frame and the ray counters bit-exact; for city 4K
-    the 8-band decomposition of configs[3] too (each band's core rows of the tone-mapped frame)."""
+    the 8-band decomposition of configs[3] too (each band's core rows of the tone-mapped frame), with
+    equal bands and with uneven (cost-balanced) ones."""
     import bench
     from hikari_amd import HikariRenderer, HikariSettings, Upscale, frame_inputs
     from hikari_amd.bands import band_of, halo_rows
@@ -96,7 +104,7 @@ def test_full_size_bench_workloads_bit_exact(config, frames):
     bands = []
     if config == "city-4k":
         for k in range(8):
-            b = band_of(k, 8, h)
+            b = band_of(k, 8, h, CITY_UNEVEN if uneven else None)
             rb = HikariRenderer(0)
             rb.set_noise()
             rb.upload_scene(scene)
@@ -114,7 +122,7 @@ def test_full_size_bench_workloads_bit_exact(config, frames):
         whole = canon_plane(10, o.output(10))
         for b, rb in bands:
             row0, rows, core0, core_rows = rb.band_info()
-            assert row0 + core0 == b.y0 and core_rows == b.rows == h // 8
+            assert row0 + core0 == b.y0 and core_rows == b.rows == (b.rows if uneven else h // 8)
             m = mismatch_report(canon_plane(10, rb.output(10)[core0: core0 + core_rows]), whole[b.y0: b.y0 + b.rows],
                                 f"frame {f} band {b.y0}+{b.rows} output 10")
             if m:

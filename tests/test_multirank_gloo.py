@@ -160,3 +160,91 @@ def test_insufficient_halo_is_detectable():
     b = band_of(0, 2, H)
     part = _render(b, 0, True, True)
     assert not np.array_equal(part[b.y0: b.y0 + b.rows], whole[b.y0: b.y0 + b.rows])
+
+
+def _balanced_worker(rank, world, port, q):
+    """bench.py's cost-balanced band wiring: every rank times its equal band, the times are all-gathered,
+    every rank computes the same new boundaries (bands.rebalance), renders its uneven band + halo from
+    frame 0, contributes it zero-padded to the largest band, and the gather is put back in frame order
+    with band_gather_rows' index."""
+    import sys
+    import time
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    for p in (root / "bevy-hikari_amd", root / "oracle", root / "tests"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    from hikari_amd.bands import band_gather_rows, band_of, equal_bounds, halo_rows, rebalance
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bounds = equal_bounds(world, H)
+    t0 = time.perf_counter()
+    _render(band_of(rank, world, H, bounds), halo_rows(True, True))
+    # a skewed cost on top of the measured one, so that the boundaries really move
+    t = torch.tensor([(time.perf_counter() - t0) * (1.0 + 3.0 * rank)], dtype=torch.float64)
+    times = torch.zeros(world, dtype=torch.float64)
+    dist.all_gather_into_tensor(times, t)
+    bounds = rebalance(bounds, times.numpy())
+    mine_b = torch.tensor(bounds, dtype=torch.int64)
+    all_b = torch.zeros(world * len(bounds), dtype=torch.int64)
+    dist.all_gather_into_tensor(all_b, mine_b)
+    band = band_of(rank, world, H, bounds)
+    img = _render(band, halo_rows(True, True))
+    pad, index = band_gather_rows(bounds)
+    mine = np.zeros((pad, W, 8), np.uint8)
+    mine[:band.rows] = img[band.y0: band.y0 + band.rows]
+    full = torch.empty((world * pad, W, 8), dtype=torch.uint8)
+    dist.all_gather_into_tensor(full, torch.from_numpy(mine))
+    if rank == 0:
+        q.put((full.numpy()[index].copy(), all_b.numpy().reshape(world, -1).tolist(), bounds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_balanced_uneven_bands_reassemble_whole_frame(world):
+    """Uneven (cost-balanced) bands: all ranks agree on the boundaries, the boundaries moved away from
+    the equal split, and the reassembled gather equals the whole-frame render."""
+    import torch.multiprocessing as mp
+    from hikari_amd.bands import equal_bounds
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, per_rank_bounds, bounds = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(b == list(bounds) for b in per_rank_bounds)
+    assert list(bounds) != equal_bounds(world, H)
+    whole = _render(None, 0, True, True)
+    assert np.array_equal(gathered, whole)
+
+
+def test_rebalance_converges_on_a_skewed_cost():
+    """bands.rebalance on a known per-row cost (city-like: the lower rows 6x as costly), each band's
+    time = its rows' cost + a fixed per-band cost: three rounds bring the slowest band within 6 % of the
+    mean, from 1.7x with equal bands; boundaries stay an increasing 8-row-aligned partition."""
+    from hikari_amd.bands import BAND_ALIGN, equal_bounds, rebalance
+    height = 2160
+    y = np.arange(height)
+    cost = 1.0 + 5.0 / (1.0 + np.exp(-(y - 1300) / 120.0))
+
+    def times(b):
+        return np.array([cost[b[k]:b[k + 1]].sum() + 40.0 for k in range(len(b) - 1)])
+
+    for world in (2, 4, 8):
+        b = equal_bounds(world, height)
+        t = times(b)
+        first = t.max() / t.mean()
+        for _ in range(3):
+            b = rebalance(b, t)
+            t = times(b)
+            assert b[0] == 0 and b[-1] == height and all(np.diff(b) >= BAND_ALIGN)
+            assert all(v % BAND_ALIGN == 0 for v in b)
+        assert first > 1.3 and t.max() / t.mean() < 1.06, (world, first, t.max() / t.mean())

@@ -11,7 +11,12 @@ The projection adds the collective: one all-gather of the tone-map
 link at ~153 GB/s (MI355X: 7 links x ~153 GB/s per GPU).  bench.py double-buffers it, so the gather of
 frame f runs on RCCL's stream next to frame f+1: frame time = max(compute, gather) when it overlaps,
 compute + gather when it does not; both are printed.
-usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N]"""
+Row bands are cost-balanced as bench.py balances them (bands.rebalance, --balance R rounds, default 2:
+every rank's band timed, the boundaries moved to equal measured cost, timed again); the equal-row split is
+printed beside it.  --overhead-ms X adds the measured per-frame cost of the collective path itself (the
+band copy, the all-gather's stream waits and the reorder at world size 1: HK_BENCH_DIST=1 minus the
+single-GPU line) to every N > 1 frame.
+usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N] [--balance R] [--overhead-ms X]"""
 import json
 import sys
 import time
@@ -24,7 +29,7 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "bevy-hikari_amd"))
 import bench  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import band_of, halo_rows, use_stripes  # noqa: E402
+from hikari_amd.bands import band_of, equal_bounds, halo_rows, rebalance, use_stripes  # noqa: E402
 
 cfg_name = sys.argv[1] if len(sys.argv) > 1 else "cornell-1080p-nee"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 50
@@ -44,14 +49,19 @@ def allgather_ms(n: int) -> float:
     return 0.0 if n == 1 else (n - 1) / n * W * H * 8 / (XGMI_LINK_GBS * 1e9) * 1e3
 
 
-out = {"config": cfg_name, "resolution": [W, H], "bands": {}, "allgather_ms": {}, "projected_ms": {}}
-only = int(sys.argv[sys.argv.index("--only") + 1]) if "--only" in sys.argv else None
-for n in (1, 2, 4, 8):
-    if only is not None and n != only:
-        continue
-    worst = 0.0
-    stripes = use_stripes(cfg["spatial"], cfg["denoise"]) and "--bands" not in sys.argv
-    for rank in sorted({0, n // 2, n - 1}):  # edge and middle bands
+def arg(name, default):
+    return type(default)(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else default
+
+
+out = {"config": cfg_name, "resolution": [W, H], "bands": {}, "allgather_ms": {}, "projected_ms": {},
+       "equal_bands": {}, "bounds": {}, "overhead_ms": arg("--overhead-ms", 0.0)}
+only = arg("--only", 0) or None
+rounds = arg("--balance", 2)
+
+
+def rank_ms(n, rank, stripes, bounds):
+    """ms/frame of rank `rank`'s rows of an N-way split, alone on the GPU."""
+    if True:
         r = HikariRenderer(0)
         r.set_noise()
         r.upload_scene(scene)
@@ -61,7 +71,7 @@ for n in (1, 2, 4, 8):
         elif stripes:
             r.resize_striped(W, H, rank, n)
         else:
-            b = band_of(rank, n, H)
+            b = band_of(rank, n, H, bounds)
             r.resize(W, H, 1.0, b.y0, b.rows)
 
         def step(f):
@@ -83,8 +93,6 @@ for n in (1, 2, 4, 8):
         ms = (time.perf_counter() - t0) / steps * 1e3
         if "--kernels" in sys.argv and rank == n // 2:
             print(f"  N={n} host enqueue {t_host / steps * 1e3:.4f} ms/frame", flush=True)
-        worst = max(worst, ms)
-        if "--kernels" in sys.argv and rank == n // 2:
             r.enable_kernel_timing(True)
             for f in range(10 + steps, 20 + steps):
                 step(f)
@@ -92,11 +100,34 @@ for n in (1, 2, 4, 8):
             print(f"  N={n} rank {rank} kernel ms:", {k: round(v, 4) for k, v in r.kernel_timing().items()}, flush=True)
             r.enable_kernel_timing(False)
         r.close()
+        return ms
+
+
+for n in (1, 2, 4, 8):
+    if only is not None and n != only:
+        continue
+    stripes = use_stripes(cfg["spatial"], cfg["denoise"]) and "--bands" not in sys.argv
+    if n == 1 or stripes:
+        worst = max(rank_ms(n, rank, stripes, None) for rank in sorted({0, n // 2, n - 1}))  # edge and middle
+    else:
+        bounds = equal_bounds(n, H)
+        times = [rank_ms(n, k, False, bounds) for k in range(n)]
+        out["equal_bands"][n] = round(max(times), 4)
+        print(f"N={n}: equal bands {[round(t, 3) for t in times]}", flush=True)
+        for _ in range(rounds):
+            bounds = rebalance(bounds, times)
+            times = [rank_ms(n, k, False, bounds) for k in range(n)]
+            print(f"N={n}: bands {bounds} -> {[round(t, 3) for t in times]}", flush=True)
+        out["bounds"][n] = [int(v) for v in bounds]
+        worst = max(times)
     out["bands"][n] = round(worst, 4)
     g = allgather_ms(n)
+    ov = out["overhead_ms"] if n > 1 else 0.0
     out["allgather_ms"][n] = round(g, 4)
-    out["projected_ms"][n] = {"overlapped": round(max(worst, g), 4), "serial": round(worst + g, 4)}
+    out["projected_ms"][n] = {"overlapped": round(max(worst, g) + ov, 4), "serial": round(worst + g + ov, 4)}
     base = out["bands"].get(1)
-    speedup = f"  speedup {base / max(worst, g):.2f}x overlapped, {base / (worst + g):.2f}x serial" if base else ""
-    print(f"N={n}: slowest band {worst:.4f} ms/frame, all-gather {g:.4f} ms{speedup}", flush=True)
+    speedup = (f"  speedup {base / (max(worst, g) + ov):.2f}x overlapped, {base / (worst + g + ov):.2f}x serial"
+               if base else "")
+    print(f"N={n}: slowest band {worst:.4f} ms/frame, all-gather {g:.4f} ms, collective-path overhead {ov:.4f} ms"
+          f"{speedup}", flush=True)
 print(json.dumps(out))
