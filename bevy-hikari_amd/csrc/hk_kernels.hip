@@ -478,15 +478,15 @@ HKD bool direct_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& C,
                                n_emitter, D.L);
     return true;
 }
-// the candidate block after its emitter walk (hit, traced: light_pick_walk's result)
+// the candidate block after its emitter walk (hit, traced: light_pick_walk's result), up to its shadow walk:
+// returns whether the shadow ray (D.ray, cand's distances) is traced
 template <bool EMISSIVE_LIT>
-HKD void direct_candidate(const FrameArgs& A, const Scene& sc, const DirectPixel& P, DirectState& D, const Hit& walk_hit,
-                          bool traced, uint32_t& n_top)
+HKD bool direct_candidate_a(const Scene& sc, const DirectPixel& P, DirectState& D, const Hit& walk_hit, bool traced,
+                            uint32_t& n_top)
 {
-    const Frame& F = A.F;
     Sample& s = D.s;
     if (D.L.emitter) light_pick_end(sc, D.L, xyz(s.visible_position), walk_hit, traced, D.info);
-    const LightCandidate cand = D.L.cand;
+    const LightCandidate& cand = D.L.cand;
     const f3 normal = P.normal;
     Ray& ray = D.ray;
     ray.origin = xyz(D.position) + normal * RAY_BIAS;
@@ -494,9 +494,18 @@ HKD void direct_candidate(const FrameArgs& A, const Scene& sc, const DirectPixel
     ray.inv_direction = inv(ray.direction);
     bool trace = dot(cand.direction, normal) > 0.0f && cand.p > 0.0f;
     if (EMISSIVE_LIT) trace = trace && cand.emissive_instance != DONT_SAMPLE_EMISSIVE;
+    if (trace) n_top++;
+    return trace;
+}
+// ... and after the shadow walk (hit: its result, when traced)
+template <bool EMISSIVE_LIT>
+HKD void direct_candidate_b(const FrameArgs& A, const Scene& sc, DirectState& D, bool trace, const Hit& hit)
+{
+    const Frame& F = A.F;
+    Sample& s = D.s;
+    const LightCandidate& cand = D.L.cand;
+    const Ray& ray = D.ray;
     if (trace) {
-        n_top++;
-        Hit hit = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
         occlude_hit_info(ray, hit, D.info);
         s.radiance = EMISSIVE_LIT ? input_radiance(sc, F, ray, D.info, false, cand.emissive_instance, false)
                                   : input_radiance(sc, F, ray, D.info, true, DONT_SAMPLE_EMISSIVE, false);
@@ -505,6 +514,15 @@ HKD void direct_candidate(const FrameArgs& A, const Scene& sc, const DirectPixel
     s.sample_normal = D.info.normal;
     float w_new = cand.p > 0.0f ? lum(xyz(s.radiance)) / cand.p : 0.0f;
     temporal_restir(D.r, s, w_new, F.max_temporal_reuse_count);
+}
+template <bool EMISSIVE_LIT>
+HKD void direct_candidate(const FrameArgs& A, const Scene& sc, const DirectPixel& P, DirectState& D, const Hit& walk_hit,
+                          bool traced, uint32_t& n_top)
+{
+    const bool trace = direct_candidate_a<EMISSIVE_LIT>(sc, P, D, walk_hit, traced, n_top);
+    Hit hit;
+    if (trace) hit = traverse_top(sc, D.ray, D.L.cand.max_distance, D.L.cand.min_distance, D.L.cand.emissive_instance);
+    direct_candidate_b<EMISSIVE_LIT>(A, sc, D, trace, hit);
 }
 
 // PARK: 0 = the validation block keeps the reservoir in registers, 1 = parks it in a static LDS array,
@@ -789,7 +807,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // and thread t runs queue entry t: the long walks of the 4 waves share one or two waves (model: 0.35).  A
 // walk's result does not depend on the thread that runs it, so the results are those of the per-pixel walk.
 constexpr uint32_t CW_LONG_NODES = 16u;
-constexpr int CW_WORDS = 9;  // request: local origin 3, direction 3, BLAS node offset, node count, primitive offset
+// LDS of a compacted batch: 9 rows of one word per thread (a request: local origin 3, direction 3, BLAS node
+// offset, node count, primitive offset; then the result over it) and a row for the queue.  With the direct
+// validation block (VD) these are rows of its park columns: a thread writes its own column's request only
+// after its own park ended, and the queue / results only after the batch's first barrier, which every
+// thread reaches after its park ended; the per-wave counts have their own array (written before it).
+constexpr int CW_WORDS = 10;
+static_assert(CW_WORDS <= PARK_WORDS, "the batch rows fit the park columns");
 HKD float* cw_area()
 {
     __shared__ float cw[CW_WORDS * 256];
@@ -798,7 +822,7 @@ HKD float* cw_area()
 // every thread of the workgroup calls this at the same point (barriers); need = the thread's pixel walks
 HKD bool compact_emitter_walks(const Scene& sc, float* lds, const LightPick& L, bool need, Hit& hit)
 {
-    __shared__ uint32_t queue[256];
+    uint32_t* const queue = reinterpret_cast<uint32_t*>(lds + 9 * 256);
     __shared__ uint32_t wave_counts[8];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint32_t node_offset = 0u, node_count = 0u;
@@ -871,12 +895,71 @@ HKD bool compact_emitter_walks(const Scene& sc, float* lds, const LightPick& L, 
     return lds[4 * 256 + t] != 0.0f;
 }
 
+// Shadow walks (traverse_top any-hit) of a workgroup as one compacted batch: the lanes that trace a shadow
+// ray are a scattered subset of the workgroup (cornell: the direct_lit pass's lanes that face the light,
+// the indirect pass's bounces that hit a surface and pick a light), and a wave with a few of them runs the
+// walk for all 64 lanes.  Requests go to LDS (origin, direction, max / early distance, excluded instance),
+// packed in pixel order, and thread t runs request t (model: cornell direct_lit 0.31 -> 0.53 of the lanes
+// busy, indirect emissive shadows 0.25 -> 0.41; tools/walk_lanes.py).  The walk's result depends only on
+// the request, so it is the per-pixel walk's.
+// (LDS: the rows of compact_emitter_walks, cw_area / park columns)
+HKD bool compact_top_walks(const Scene& sc, float* lds, bool need, const Ray& ray, float max_distance, float early_distance,
+                           uint32_t exclude, Hit& hit)
+{
+    uint32_t* const ct_queue = reinterpret_cast<uint32_t*>(lds + 9 * 256);
+    __shared__ uint32_t ct_counts[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    if (need) {
+        lds[0 * 256 + t] = ray.origin.x;
+        lds[1 * 256 + t] = ray.origin.y;
+        lds[2 * 256 + t] = ray.origin.z;
+        lds[3 * 256 + t] = ray.direction.x;
+        lds[4 * 256 + t] = ray.direction.y;
+        lds[5 * 256 + t] = ray.direction.z;
+        lds[6 * 256 + t] = max_distance;
+        lds[7 * 256 + t] = early_distance;
+        lds[8 * 256 + t] = __uint_as_float(exclude);
+    }
+    const uint64_t m = __ballot(need);
+    if (lane == 0u) ct_counts[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t n = 0u, below = 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+        const uint32_t a = ct_counts[k];
+        below += k < w ? a : 0u;
+        n += a;
+    }
+    if (need) ct_queue[below + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = t;
+    __syncthreads();
+    if (t < n) {
+        const uint32_t o = ct_queue[t];
+        Ray r;
+        r.origin = mk3(lds[0 * 256 + o], lds[1 * 256 + o], lds[2 * 256 + o]);
+        r.direction = mk3(lds[3 * 256 + o], lds[4 * 256 + o], lds[5 * 256 + o]);
+        r.inv_direction = inv(r.direction);
+        const Hit h = traverse_top(sc, r, lds[6 * 256 + o], lds[7 * 256 + o], __float_as_uint(lds[8 * 256 + o]));
+        lds[0 * 256 + o] = h.uv.x;
+        lds[1 * 256 + o] = h.uv.y;
+        lds[2 * 256 + o] = h.distance;
+        lds[3 * 256 + o] = __uint_as_float(h.instance_index);
+        lds[4 * 256 + o] = __uint_as_float(h.primitive_index);
+    }
+    __syncthreads();
+    if (!need) return false;
+    hit.uv = mk2(lds[0 * 256 + t], lds[1 * 256 + t]);
+    hit.distance = lds[2 * 256 + t];
+    hit.instance_index = __float_as_uint(lds[3 * 256 + t]);
+    hit.primitive_index = __float_as_uint(lds[4 * 256 + t]);
+    return true;
+}
+
 // k_direct_fused_w4 on the frames that validate neither pass's emitter picks (VE false) with the emissive
 // pass's emitter walks compacted per workgroup (compact_emitter_walks).  Every thread reaches the barriers:
 // the pixel's work is predicated, not returned from.  The walk requests live in the direct validation
 // block's park columns when that block runs (VD: a thread's own column, written after its own block ended)
 // or in their own LDS array.
-template <bool VD>
+template <bool VD, bool SHADOW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_fused_cw(FrameArgs A, ChannelArgs C0,
                                                                                                    ChannelArgs C1)
 {
@@ -900,13 +983,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     Surface surface;
     DirectState D;
     bool lit = false;
-    if (work) {
+    if constexpr (SHADOW) {
+        // direct_lit with its candidate block's shadow walk compacted (its validation block, every
+        // direct_validate_interval-th frame, walks per pixel)
+        bool cand = false, trace = false;
+        if (work) {
+            lit = direct_begin<false, true, VD>(A, sc, C0, P, D, n_emitter);
+            cand = lit && D.cand_block;
+            Hit none;
+            if (cand) trace = direct_candidate_a<false>(sc, P, D, none, false, n_top);
+        }
+        Hit sh;
+        compact_top_walks(sc, lds, trace, D.ray, D.L.cand.max_distance, D.L.cand.min_distance, D.L.cand.emissive_instance, sh);
+        if (cand) direct_candidate_b<false>(A, sc, D, trace, sh);
+        if (lit) direct_finish<false, true, VD, 1>(A, sc, C0, P, D, n_top, n_emitter, &surface);
+        lit = false;
+        if (work) lit = direct_begin<true, false, false>(A, sc, C1, P, D, n_emitter);
+    } else if (work) {
         direct_body<false, true, VD, 1>(A, sc, C0, P, n_top, n_emitter, &surface);
         lit = direct_begin<true, false, false>(A, sc, C1, P, D, n_emitter);
     }
     Hit hit;
     const bool traced = compact_emitter_walks(sc, lds, D.L, lit && D.L.walk, hit);
-    if (lit) {
+    if constexpr (SHADOW) {
+        bool trace = false;
+        if (lit) trace = direct_candidate_a<true>(sc, P, D, hit, traced, n_top);
+        Hit sh;
+        compact_top_walks(sc, lds, trace, D.ray, D.L.cand.max_distance, D.L.cand.min_distance, D.L.cand.emissive_instance, sh);
+        if (lit) {
+            direct_candidate_b<true>(A, sc, D, trace, sh);
+            direct_finish<true, false, false, 0>(A, sc, C1, P, D, n_top, n_emitter, nullptr, &surface);
+        }
+    } else if (lit) {
         direct_candidate<true>(A, sc, P, D, hit, traced, n_top);
         direct_finish<true, false, false, 0>(A, sc, C1, P, D, n_top, n_emitter, nullptr, &surface);
     }
@@ -937,12 +1045,89 @@ HKD Hit wf_load_hit(const WfArgs& W, int32_t idx)
     h.distance = W.hit_t[idx];
     return h;
 }
-// returns (IND_GEN) whether the pixel traces a bounce; (IND_TRACE) the hit's material bin in *key
+// indirect_lit_ambient's one-bounce path (light.wgsl:1300-1394 with indirect_bounces 1) in pieces around its
+// two walks, so that a kernel can run the shadow walks of a workgroup as one compacted batch (k_indirect's CS
+// variant): bounce_ray builds the cosine bounce, bounce_hit_a runs everything from the bounce's hit to the
+// shadow ray (hit_info, the hit's surface, select_light_candidate), bounce_hit_b everything after the shadow
+// walk.  indirect_body runs them with the walks in between: the same statements in the same order.
+struct BounceState {
+    Sample s;
+    Ray ray;
+    HitInfo info;
+    Surface surface;
+    LightCandidate cand;
+    bool hit, sample_directional;
+};
+HKD f4 bounce_ray(BounceState& B)
+{
+    const Sample& s = B.s;
+    f4 rs = sample_cosine_hemisphere(mk2(s.random.x, s.random.y));
+    B.ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
+    f3 bt, bb;
+    normal_basis(s.visible_normal, bt, bb);
+    B.ray.direction = basis_mul(bt, bb, s.visible_normal, xyz(rs));
+    B.ray.inv_direction = inv(B.ray.direction);
+    return rs;
+}
+// returns whether the shadow ray (B.ray, B.cand's distances and instance) is traced
+HKD bool bounce_hit_a(const Scene& sc, const Frame& F, BounceState& B, const Hit& hit, uint32_t& n_top, uint32_t& n_emitter)
+{
+    Sample& s = B.s;
+    HitInfo& info = B.info;
+    info = hit_info(sc, B.ray, hit);
+    s.sample_position = info.position;
+    s.sample_normal = info.normal;
+    B.hit = hit.instance_index != HK_U32_MAX;
+    if (!B.hit) return false;
+    B.surface = retreive_surface(sc, info.material_index, info.uv);
+    B.surface.roughness = 1.0f;
+    B.cand = select_light_candidate<true>(sc, F, s.random, xyz(s.sample_position), s.sample_normal, info.instance_index,
+                                          info, n_emitter);
+    B.sample_directional = B.cand.emissive_instance == DONT_SAMPLE_EMISSIVE;
+    if (!(dot(B.cand.direction, s.sample_normal) > 0.0f && B.cand.p > 0.0f)) return false;
+    B.ray.origin = xyz(s.sample_position) + s.sample_normal * RAY_BIAS;
+    B.ray.direction = B.cand.direction;
+    B.ray.inv_direction = inv(B.ray.direction);
+    n_top++;
+    return true;
+}
+HKD void bounce_hit_b(const Scene& sc, const Frame& F, BounceState& B, bool shadow, const Hit& sh)
+{
+    Sample& s = B.s;
+    if (B.hit) {
+        if (shadow) {
+            occlude_hit_info(B.ray, sh, B.info);
+            f4 in_rad = input_radiance(sc, F, B.ray, B.info, B.sample_directional, B.cand.emissive_instance, false);
+            f3 out = shading(F, normalize(xyz(s.visible_position) - xyz(s.sample_position)), s.sample_normal,
+                             B.ray.direction, B.surface, in_rad);
+            out = out / B.cand.p;
+            s.radiance = mk4(s.radiance.x + out.x, s.radiance.y + out.y, s.radiance.z + out.z, s.radiance.w + 1.0f);
+        }
+    } else {
+        f3 out = xyz(input_radiance(sc, F, B.ray, B.info, false, DONT_SAMPLE_EMISSIVE, true));
+        s.radiance = mk4(s.radiance.x + out.x, s.radiance.y + out.y, s.radiance.z + out.z, s.radiance.w + 0.0f);
+    }
+}
+
+// The pass up to the one-bounce path's shadow walk (I.shadow: whether it is traced; the multiple-bounce
+// path runs its whole loop here).  Returns false when the pixel's pass ends here: a background pixel (its
+// stores done), the IND_GEN / IND_TRACE stages (*ret: their result).
+struct IndirectState {
+    BounceState B;
+    int32_t idx;
+    f2 uv;
+    f4 position, velocity_uv;
+    uint32_t im_y;
+    float pdf;
+    bool shadow;
+};
 template <bool MULTI, int STAGE = IND_ALL>
-HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
-                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr)
+HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
+                        uint32_t& n_emitter, const WfArgs* W, uint32_t* key, IndirectState& I, bool& ret)
 {
     static_assert(!MULTI || STAGE == IND_ALL, "the wavefront stages cover one bounce");
+    I.shadow = false;
+    ret = false;
     const Frame& F = A.F;
     const int32_t idx = s_index(F, x, y);
     const f2 uv = coords_to_uv(x, y, F.s);
@@ -970,7 +1155,10 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
         }
         return false;
     }
-    if constexpr (STAGE == IND_GEN) return true;
+    if constexpr (STAGE == IND_GEN) {
+        ret = true;
+        return false;
+    }
     f3 normal = normalize(load_normal(F, A.G, dx, dy));
     f2 imf = load_instance_material(F, A.G, dx, dy);
     uint32_t im_x = f2u32(imf.x), im_y = f2u32(imf.y);
@@ -1044,52 +1232,50 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
             }
         }
     } else {
-        f4 rs = sample_cosine_hemisphere(mk2(s.random.x, s.random.y));
-        ray.origin = xyz(s.visible_position) + s.visible_normal * RAY_BIAS;
-        f3 bt, bb;
-        normal_basis(s.visible_normal, bt, bb);
-        ray.direction = basis_mul(bt, bb, s.visible_normal, xyz(rs));
-        ray.inv_direction = inv(ray.direction);
+        BounceState B;
+        B.s = s;
+        B.ray = ray;
         Hit hit;
+        const f4 rs = bounce_ray(B);
         if constexpr (STAGE == IND_SHADE) {
             hit = wf_load_hit(*W, idx);
         } else {
             n_top++;
-            hit = traverse_top(sc, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+            hit = traverse_top(sc, B.ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
         }
         if constexpr (STAGE == IND_TRACE) {
             wf_store_hit(*W, idx, hit);
             *key = hit.instance_index != HK_U32_MAX ? min(get_instance(sc, hit.instance_index).material, W->bins - 2u) : W->bins - 1u;
-            return true;
+            ret = true;
+            return false;
         }
-        info = hit_info(sc, ray, hit);
-        s.sample_position = info.position;
-        s.sample_normal = info.normal;
         pdf = rs.w;
-        if (hit.instance_index != HK_U32_MAX) {
-            surface = retreive_surface(sc, info.material_index, info.uv);
-            surface.roughness = 1.0f;
-            LightCandidate cand = select_light_candidate<true>(sc, F, s.random, xyz(s.sample_position), s.sample_normal,
-                                                               info.instance_index, info, n_emitter);
-            bool sample_directional = cand.emissive_instance == DONT_SAMPLE_EMISSIVE;
-            if (dot(cand.direction, s.sample_normal) > 0.0f && cand.p > 0.0f) {
-                ray.origin = xyz(s.sample_position) + s.sample_normal * RAY_BIAS;
-                ray.direction = cand.direction;
-                ray.inv_direction = inv(ray.direction);
-                n_top++;
-                Hit sh = traverse_top(sc, ray, cand.max_distance, cand.min_distance, cand.emissive_instance);
-                occlude_hit_info(ray, sh, info);
-                f4 in_rad = input_radiance(sc, F, ray, info, sample_directional, cand.emissive_instance, false);
-                f3 out = shading(F, normalize(xyz(s.visible_position) - xyz(s.sample_position)), s.sample_normal,
-                                 ray.direction, surface, in_rad);
-                out = out / cand.p;
-                s.radiance = mk4(s.radiance.x + out.x, s.radiance.y + out.y, s.radiance.z + out.z, s.radiance.w + 1.0f);
-            }
-        } else {
-            f3 out = xyz(input_radiance(sc, F, ray, info, false, DONT_SAMPLE_EMISSIVE, true));
-            s.radiance = mk4(s.radiance.x + out.x, s.radiance.y + out.y, s.radiance.z + out.z, s.radiance.w + 0.0f);
-        }
+        I.shadow = bounce_hit_a(sc, F, B, hit, n_top, n_emitter);
+        I.B = B;
     }
+    if (MULTI) I.B.s = s;
+    I.idx = idx;
+    I.uv = uv;
+    I.position = position;
+    I.velocity_uv = velocity_uv;
+    I.im_y = im_y;
+    I.pdf = pdf;
+    return true;
+}
+// the rest of the pass after the shadow walk (sh: its result when I.shadow)
+template <bool MULTI>
+HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, IndirectState& I, const Hit& sh)
+{
+    const Frame& F = A.F;
+    if (!MULTI) bounce_hit_b(sc, F, I.B, I.shadow, sh);
+    Sample& s = I.B.s;
+    const int32_t idx = I.idx;
+    const f2 uv = I.uv;
+    const f4 position = I.position, velocity_uv = I.velocity_uv;
+    const uint32_t im_y = I.im_y;
+    const float pdf = I.pdf;
+    Reservoir r;
+    Surface surface;
 
     f2 juv = jittered_uv(F, uv, 0.25f);
     f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
@@ -1116,10 +1302,24 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
     if (F.temporal_reuse > 0u) store_res_view(C.cur, C.view, C.view_n, idx, r);
     f3 o = out * r.w;
     store_rgba16f(C.render, idx, mk4(o.x, o.y, o.z, 1.0f));
+}
+// returns (IND_GEN) whether the pixel traces a bounce; (IND_TRACE) the hit's material bin in *key
+template <bool MULTI, int STAGE = IND_ALL>
+HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
+                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr)
+{
+    IndirectState I;
+    bool ret;
+    if (!indirect_begin<MULTI, STAGE>(A, sc, C, x, y, n_top, n_emitter, W, key, I, ret)) return ret;
+    Hit sh;
+    if (!MULTI && I.shadow)
+        sh = traverse_top(sc, I.B.ray, I.B.cand.max_distance, I.B.cand.min_distance, I.B.cand.emissive_instance);
+    indirect_end<MULTI>(A, sc, C, I, sh);
     return true;
 }
 
-template <bool MULTI, bool LDS>
+// CS: the one-bounce path's shadow walks compacted per workgroup (compact_top_walks; option compact_shadow)
+template <bool MULTI, bool LDS, bool CS = false>
 __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
@@ -1129,7 +1329,17 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, C
         sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     }
     uint32_t n_top = 0, n_emitter = 0;
-    if (active) indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+    if constexpr (CS && !MULTI) {
+        IndirectState I;
+        bool ret = false;
+        const bool live = active && indirect_begin<false>(A, sc, C, x, y, n_top, n_emitter, nullptr, nullptr, I, ret);
+        Hit sh;
+        compact_top_walks(sc, cw_area(), live && I.shadow, I.B.ray, I.B.cand.max_distance, I.B.cand.min_distance,
+                          I.B.cand.emissive_instance, sh);
+        if (live) indirect_end<false>(A, sc, C, I, sh);
+    } else if (active) {
+        indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+    }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -1993,9 +2203,13 @@ static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const Chan
                            uint32_t lds, hipStream_t st)
 {
     const bool w4 = A.opt.fused_w4 != 0;
-    if (!LDS && w4 && !ve && A.opt.compact_emitter) {
-        if (vd) hipLaunchKernelGGL((k_direct_fused_cw<true>), g, dim3(256), lds, st, A, C0, C1);
-        else hipLaunchKernelGGL((k_direct_fused_cw<false>), g, dim3(256), lds, st, A, C0, C1);
+    if (!LDS && w4 && !ve && (A.opt.compact_emitter || A.opt.compact_shadow)) {
+        // (compact_shadow implies the emitter compaction: one kernel variant per shadow choice)
+        if (A.opt.compact_shadow) {
+            if (vd) hipLaunchKernelGGL((k_direct_fused_cw<true, true>), g, dim3(256), lds, st, A, C0, C1);
+            else hipLaunchKernelGGL((k_direct_fused_cw<false, true>), g, dim3(256), lds, st, A, C0, C1);
+        } else if (vd) hipLaunchKernelGGL((k_direct_fused_cw<true, false>), g, dim3(256), lds, st, A, C0, C1);
+        else hipLaunchKernelGGL((k_direct_fused_cw<false, false>), g, dim3(256), lds, st, A, C0, C1);
     } else if (!LDS && w4 && ve) {
         if (vd) hipLaunchKernelGGL((k_direct_fused_w4<LDS, true, true>), g, dim3(256), lds, st, A, C0, C1);
         else hipLaunchKernelGGL((k_direct_fused_w4<LDS, false, true>), g, dim3(256), lds, st, A, C0, C1);
@@ -2074,6 +2288,9 @@ void launch_indirect(const FrameArgs& A, const ChannelArgs& C, bool multi, hipSt
     if (multi) {
         if (lds) hipLaunchKernelGGL((k_indirect<true, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_indirect<true, false>), g, dim3(256), 0, st, A, C);
+    } else if (A.opt.compact_shadow) {
+        if (lds) hipLaunchKernelGGL((k_indirect<false, true, true>), g, dim3(256), lds, st, A, C);
+        else hipLaunchKernelGGL((k_indirect<false, false, true>), g, dim3(256), 0, st, A, C);
     } else {
         if (lds) hipLaunchKernelGGL((k_indirect<false, true>), g, dim3(256), lds, st, A, C);
         else hipLaunchKernelGGL((k_indirect<false, false>), g, dim3(256), 0, st, A, C);

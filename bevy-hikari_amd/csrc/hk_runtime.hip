@@ -57,6 +57,7 @@ enum Opt {
     OPT_FUSED_W4,
     OPT_PERSISTENT_INDIRECT,
     OPT_COMPACT_EMITTER,
+    OPT_COMPACT_SHADOW,
     OPT_COUNT
 };
 struct OptDef {
@@ -70,7 +71,7 @@ constexpr OptDef OPTS[OPT_COUNT] = {
     {"band_full_windows", 0, 0, 1},        {"leaf_collapse", 1, 0, 1},     {"gbuffer_reuse", 1, 0, 1},
     {"lds_scene", 1, 0, 2},                {"gbuffer_stack_full", 0, 0, 1}, {"gbuffer_deep", 0, 0, 1},
     {"direct_w4_min_px", 4e5, 0.0, 1e12},  {"fused_w4", 1, 0, 1},          {"persistent_indirect", 0, 0, 1},
-    {"compact_emitter", 1, 0, 1},
+    {"compact_emitter", 1, 0, 1},          {"compact_shadow", 0, 0, 1},
 };
 }  // namespace
 
@@ -634,6 +635,7 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.opt.fused_w4 = c->on(OPT_FUSED_W4);
     A.opt.persistent_indirect = c->on(OPT_PERSISTENT_INDIRECT);
     A.opt.compact_emitter = c->on(OPT_COMPACT_EMITTER);
+    A.opt.compact_shadow = c->on(OPT_COMPACT_SHADOW);
     return A;
 }
 

@@ -217,6 +217,7 @@ void hk_settings_default(hk_settings* out);
  *   persistent_indirect (0)  kernel-variant choices (tests force each variant with them)
  *   compact_emitter (1)      the fused direct/emissive launch runs a workgroup's emitter BLAS walks as one
  *                            compacted batch (long walks first) on frames without emissive validation
+ *   compact_shadow (0)       shadow walks of a workgroup as one compacted batch (fused launch, indirect pass)
  * hk_set_option returns HK_ERR_INVALID for an unknown key or a value outside the key's range. */
 int hk_set_option(hk_ctx* ctx, const char* key, double value);
 int hk_get_option(const hk_ctx* ctx, const char* key, double* value);

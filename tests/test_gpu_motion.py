@@ -291,7 +291,8 @@ def test_forced_kernel_variants_bit_exact(hk_options, lds):
     """Kernel variants the size thresholds normally pick only at large sizes, forced on a small
     frame: k_direct_lit_w4 (4 waves per SIMD; direct_w4_min_px=0 with fuse=0), the fused
     direct+emissive launch next to the indirect side stream (fuse_min_px=0, merge=0; its emitter walks
-    compacted per workgroup, and with compact_emitter=0 per pixel) and the
+    compacted per workgroup, and with compact_emitter=0 per pixel, with compact_shadow=1 its shadow walks
+    compacted too) and the
     merged direct+indirect launch (k_light_merged, merge=1: the default only for small frames without
     spatial reuse; here with spatial reuse after it) and the persistent-wave indirect pass
     (k_indirect_persist, persistent_indirect=1, an opt-in), each with and without LDS scene staging."""
@@ -302,6 +303,7 @@ def test_forced_kernel_variants_bit_exact(hk_options, lds):
     s = st.to_c()
     for env in ({"direct_w4_min_px": 0, "fuse": 0}, {"fuse_min_px": 0, "merge": 0},
                 {"fuse_min_px": 0, "merge": 0, "compact_emitter": 0},
+                {"fuse_min_px": 0, "merge": 0, "compact_shadow": 1},
                 {"merge": 1}, {"persistent_indirect": 1, "merge": 0}):
         hk_options.clear()
         hk_options.update(lds_scene=int(lds), **env)
