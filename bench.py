@@ -119,7 +119,8 @@ CONFIGS = {
                                      "emissive sphere: GPU instance/TLAS/light-BVH rebuild every frame"),
     # configs[1] / configs[3] under camera motion: the examples' orbit camera (OrbitCameraBundle,
     # cornell.rs:56-60, city.rs:134-138) yawing 0.5 deg per frame (examples.orbit).  Reprojection is no
-    # longer the identity, so the fused direct/emissive launch and background store elision are off
+    # longer the identity, so the fused direct/emissive launch is off and the direct pair's background stores
+    # stay; background store elision of each pass's own targets (and of the indirect pair) stays on
     "cornell-1080p-nee-orbit": dict(scene="cornell", width=1920, height=1080, spatial=False, denoise=False, orbit=True,
                                     workload="examples/cornell.rs 1920x1080 1spp, traversal + NEE only, orbit "
                                              "camera (0.5 deg/frame)"),
@@ -258,6 +259,10 @@ def main():
     dist_on = world > 1 or os.environ.get("HK_BENCH_DIST") == "1"
     device = 0 if rehearsal else local
     torch.cuda.set_device(device)
+    # the context first: HIP maps streams onto the process's hardware queues in creation order, and the
+    # context's streams are tuned for the mapping they get when nothing else created streams before them
+    # (DESIGN §4); RCCL's communicator (created eagerly below) and torch's stream pool come after
+    r = HikariRenderer(device)
     if dist_on:
         if rehearsal:
             dist.init_process_group("gloo")
@@ -274,7 +279,6 @@ def main():
 
     # rows of this rank (hikari_amd/bands.py): interleaved stripes, or a contiguous band + halo
     stripes = dist_on and use_stripes(cfg["spatial"], cfg["denoise"])
-    r = HikariRenderer(device)
     # HK_BENCH_OPTS="key=value,..." (or "+"-separated): runtime options (hk_set_option) for A/B runs (tools/ab.sh); the
     # defaults are the tuned configuration
     bench_opts = {kv.split("=")[0]: float(kv.split("=")[1])
@@ -352,6 +356,12 @@ def main():
 
     spp = cfg.get("spp", 1)
     shown = hikari_amd._abi.OUT_TONE_MAPPED if spp == 1 else hikari_amd._abi.OUT_ACCUMULATED
+    # 1-spp frames gather frame f's rows after frame f + 1 has been queued (HK_OUT_TONE_MAPPED_PREVIOUS): the
+    # copy and the all-gather wait for frame f's tail, and their wait packets sit in hardware queues that the
+    # context's streams share (4 queues per process); queued behind frame f + 1's passes they hold back only
+    # frame f + 2's work, by which time frame f's tail has long ended.  Queued right after frame f, they held
+    # frame f + 1's G-buffer and light passes until frame f's tail ended (cornell world-1 0.58 vs 0.43 ms).
+    delay = spp == 1
 
     # camera of frame f and of frame f - 1 (None: static, PreviousViewUniform = the current view)
     if cfg.get("orbit"):
@@ -391,29 +401,40 @@ def main():
         if spp > 1:
             r.resolve_accumulation(sp)
         if dist_on:
-            k = f & 1
-            with torch.cuda.stream(comm):
-                if pending[k] is not None:
-                    pending[k].wait()  # device-side: the comm stream waits for that gather
-                if reorder and reorder_done[k] is not None:
-                    comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
-                r.copy_output_rows(shown, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
-                if rehearsal:
-                    parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
-                    dist.all_gather(parts, band_t[k].cpu())
-                    full_t[k].copy_(torch.cat(parts))
-                else:
-                    pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
-            if reorder:
-                with torch.cuda.stream(side):
-                    if pending[k] is not None:
-                        pending[k].wait()
-                    else:
-                        side.wait_stream(comm)
-                    torch.index_select(full_t[k], 0, index_t, out=frame_t[k])
-                    reorder_done[k] = side.record_event()
+            if not delay:
+                gather(f, shown)
+            elif f - 1 > gathered[0]:
+                gather(f - 1, hikari_amd._abi.OUT_TONE_MAPPED_PREVIOUS)
 
-    def drain():
+    gathered = [-1]  # the latest frame whose rows were gathered
+
+    def gather(f, plane):
+        gathered[0] = f
+        k = f & 1
+        with torch.cuda.stream(comm):
+            if pending[k] is not None:
+                pending[k].wait()  # device-side: the comm stream waits for that gather
+            if reorder and reorder_done[k] is not None:
+                comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
+            r.copy_output_rows(plane, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
+            if rehearsal:
+                parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
+                dist.all_gather(parts, band_t[k].cpu())
+                full_t[k].copy_(torch.cat(parts))
+            else:
+                pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
+        if reorder:
+            with torch.cuda.stream(side):
+                if pending[k] is not None:
+                    pending[k].wait()
+                else:
+                    side.wait_stream(comm)
+                torch.index_select(full_t[k], 0, index_t, out=frame_t[k])
+                reorder_done[k] = side.record_event()
+
+    def drain(last):
+        if delay and last > gathered[0]:  # the last queued frame's rows (no frame follows it)
+            gather(last, shown)
         for k in range(2):
             if pending[k] is not None:
                 pending[k].wait()
@@ -425,7 +446,7 @@ def main():
     for f in range(args.warmup):
         step(f)
     if dist_on:
-        drain()
+        drain(args.warmup - 1)
         dist.barrier()
     torch.cuda.synchronize()
     r.reset_counters()
@@ -441,7 +462,7 @@ def main():
     for f in range(args.warmup, args.warmup + args.steps):
         step(f)
     if dist_on:
-        drain()  # every timed frame's gather is complete inside the timed region
+        drain(args.warmup + args.steps - 1)  # every timed frame's gather is complete inside the timed region
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -582,6 +603,9 @@ def main():
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), file=out, flush=True)
+    if dist_on:
+        drain(-1)
+        torch.cuda.synchronize()
     r.close()
     if dist_on:
         dist.destroy_process_group()

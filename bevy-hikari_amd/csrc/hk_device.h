@@ -508,6 +508,13 @@ HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
 // results are unchanged; a tested neighbour costs one 16-B gather instead of two and a merged one two or
 // three instead of four.
 constexpr uint32_t VIEW_HIT = 1u << 24, VIEW_COUNT = 1u << 25;
+// HK_VIEW_AOS (experiment builds): the three chunks of a pixel in one 64-byte line (4 x uint4, the fourth
+// unused) instead of three planes, so a merged neighbour's two or three gathers fall in one cache line
+#ifndef HK_VIEW_AOS
+#define HK_VIEW_AOS 0
+#endif
+constexpr uint32_t VIEW_PLANES = HK_VIEW_AOS ? 4u : 3u;  // uint4 chunks allocated per pixel
+HKD uint32_t view_at(uint32_t view_n, uint32_t plane, uint32_t u) { return HK_VIEW_AOS ? 4u * u + plane : plane * view_n + u; }
 HKD void store_res_view(const ResBuf& b, uint4* view, uint32_t view_n, int32_t i, const Reservoir& r)
 {
     uint4 c0, c1, c2, c3;
@@ -523,11 +530,11 @@ HKD void store_res_view(const ResBuf& b, uint4* view, uint32_t view_n, int32_t i
                            (!(unpack_lo16float(c3.z) < HK_F32_EPSILON) ? VIEW_COUNT : 0u);
     const float rand = hk_fract(((hk_unpack_unorm16_fast(c0.z) + hk_unpack_unorm16_fast(c0.z >> 16)) +
                                  hk_unpack_unorm16_fast(c0.w)) + hk_unpack_unorm16_fast(c0.w >> 16));
-    view[u] = make_uint4(c2.x, c2.y, c2.z, (c3.x & 0x00FFFFFFu) | flags);
+    view[view_at(view_n, 0u, u)] = make_uint4(c2.x, c2.y, c2.z, (c3.x & 0x00FFFFFFu) | flags);
     // spatial reuse reads plane 1 only behind VIEW_COUNT and plane 2 only behind VIEW_HIT (plane 0 of the
     // same frame), so a chunk whose flag is clear is never read and its store is skipped
-    if (flags & VIEW_COUNT) view[view_n + u] = make_uint4(c0.x, c0.y, c3.z, __float_as_uint(rand));
-    if (flags & VIEW_HIT) view[2u * view_n + u] = make_uint4(c1.x, c1.y, c1.z, c3.y);
+    if (flags & VIEW_COUNT) view[view_at(view_n, 1u, u)] = make_uint4(c0.x, c0.y, c3.z, __float_as_uint(rand));
+    if (flags & VIEW_HIT) view[view_at(view_n, 2u, u)] = make_uint4(c1.x, c1.y, c1.z, c3.y);
 }
 
 HKD void set_reservoir(Reservoir& r, const Sample& s, float w_new)

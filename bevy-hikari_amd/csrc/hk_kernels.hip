@@ -1618,9 +1618,15 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_wf_shade(FrameArgs A, C
 // loads per pixel.  Values are load_depth() of the same coordinates (frame-OOB -> 0, band
 // clamp), so results are unchanged; a coordinate outside the window reads global memory.
 constexpr int32_t SP_HALO = 22, SP_WIN = 16 + 2 * SP_HALO;
+// HK_SP_P0WIN (experiment builds): the indirect spatial pass also stages view plane 0 of its window in LDS
+// (57.6 KiB per workgroup besides the depth window: 2 workgroups per CU instead of 5)
+#ifndef HK_SP_P0WIN
+#define HK_SP_P0WIN 0
+#endif
 struct DepthWin {
     const float* lds;  // null: no window (upscale ratio != 1)
     int32_t x0, y0;
+    const uint4* p0;   // HK_SP_P0WIN: view plane 0 of the window, or null
 };
 HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t x, int32_t y)
 {
@@ -1790,7 +1796,8 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         bool count_ok;
         f3 q_sample;
         if constexpr (VIEW) {
-            const uint4 a = C.view[nidx];
+            const uint4 a = (HK_SP_P0WIN && WINDOW) ? W.p0[(scy - W.y0) * SP_WIN + (scx - W.x0)]
+                                                    : C.view[view_at(C.view_n, 0u, (uint32_t)nidx)];
             normal_word = a.w;
             count_ok = (a.w & VIEW_COUNT) != 0u;
             q_sample = mk3(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
@@ -1818,7 +1825,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         f4 q_radiance;
         bool hit;
         if constexpr (VIEW) {
-            const uint4 b = C.view[C.view_n + (uint32_t)nidx];
+            const uint4 b = C.view[view_at(C.view_n, 1u, (uint32_t)nidx)];
             q_radiance = mk4(unpack_lo16float(b.x), unpack_hi16float(b.x), unpack_lo16float(b.y), unpack_hi16float(b.y));
             q_count = unpack_lo16float(b.z);
             q_w = unpack_hi16float(b.z);
@@ -1841,7 +1848,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             uint4 c1;
             uint32_t sample_normal_word;
             if constexpr (VIEW) {
-                c1 = C.view[2u * C.view_n + (uint32_t)nidx];
+                c1 = C.view[view_at(C.view_n, 2u, (uint32_t)nidx)];
                 sample_normal_word = c1.w;
             } else {
                 c1 = C.cur.base[res_chunk(C.cur, 1u, (uint32_t)nidx)];
@@ -1910,7 +1917,8 @@ template <bool EMISSIVE_LIT, bool WINDOW, bool VIEW>
 __global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, ChannelArgs C)
 {
     __shared__ float win[WINDOW ? SP_WIN * SP_WIN : 1];
-    DepthWin W{nullptr, 0, 0};
+    __shared__ uint4 p0win[(HK_SP_P0WIN && WINDOW && VIEW) ? SP_WIN * SP_WIN : 1];
+    DepthWin W{nullptr, 0, 0, nullptr};
     if (WINDOW) {
         int32_t x0, y0;
         tile_origin<HK_SPATIAL_ORDER>(A.F, A.F.s_row0, x0, y0);
@@ -1918,6 +1926,15 @@ __global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, Cha
         W.y0 = y0 - SP_HALO;
         for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256)
             win[k] = load_depth(A.F, A.G, W.x0 + k % SP_WIN, W.y0 + k / SP_WIN);
+        if constexpr (HK_SP_P0WIN && VIEW) {
+            for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256) {
+                const int32_t wx = W.x0 + k % SP_WIN, wy = W.y0 + k / SP_WIN;
+                // the neighbour test's frame bounds; s_index clamps to the band's rows as the gather does
+                const bool in = wx >= 0 && wy >= 0 && wx < (int32_t)A.F.s[0] && wy < (int32_t)A.F.s[1];
+                p0win[k] = in ? C.view[view_at(C.view_n, 0u, (uint32_t)s_index(A.F, wx, wy))] : make_uint4(0, 0, 0, 0);
+            }
+            W.p0 = p0win;
+        }
         __syncthreads();
         W.lds = win;
     }

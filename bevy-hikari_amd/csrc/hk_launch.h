@@ -19,7 +19,7 @@ struct LaunchOpts {
     double direct_w4_min_px = 4e5;   // ("direct_w4_min_px") k_direct_lit_w4 from this many pixels up
     int fused_w4 = 1;                // ("fused_w4") the 4-wave fused direct/emissive variants
     int persistent_indirect = 0;     // ("persistent_indirect") k_indirect_persist (opt-in, measured slower)
-    int compact_emitter = 1;         // ("compact_emitter") the fused launch's emitter walks compacted per workgroup
+    int compact_emitter = 0;         // ("compact_emitter") the fused launch's emitter walks compacted per workgroup
     int compact_shadow = 0;          // ("compact_shadow") shadow walks compacted per workgroup (fused launch, indirect)
 };
 

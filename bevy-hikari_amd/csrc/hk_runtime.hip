@@ -71,7 +71,7 @@ constexpr OptDef OPTS[OPT_COUNT] = {
     {"band_full_windows", 0, 0, 1},        {"leaf_collapse", 1, 0, 1},     {"gbuffer_reuse", 1, 0, 1},
     {"lds_scene", 1, 0, 2},                {"gbuffer_stack_full", 0, 0, 1}, {"gbuffer_deep", 0, 0, 1},
     {"direct_w4_min_px", 4e5, 0.0, 1e12},  {"fused_w4", 1, 0, 1},          {"persistent_indirect", 0, 0, 1},
-    {"compact_emitter", 1, 0, 1},          {"compact_shadow", 0, 0, 1},
+    {"compact_emitter", 0, 0, 1},          {"compact_shadow", 0, 0, 1},
 };
 }  // namespace
 
@@ -1223,8 +1223,8 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     }
     HK_HIP(c, hipMalloc(&c->gbmask, SP));
     c->gb_valid = false;
-    HK_HIP(c, hipMalloc(&c->sp_view, 3 * sp * sizeof(uint4)));
-    HK_HIP(c, hipMemset(c->sp_view, 0, 3 * sp * sizeof(uint4)));
+    HK_HIP(c, hipMalloc(&c->sp_view, VIEW_PLANES * sp * sizeof(uint4)));
+    HK_HIP(c, hipMemset(c->sp_view, 0, VIEW_PLANES * sp * sizeof(uint4)));
     for (int ch = 0; ch < 3; ++ch) {
         for (int i = 0; i < 4; ++i) {
             HK_HIP(c, hipMalloc(&c->internal[ch][i], sp * sizeof(uint2)));
@@ -1912,6 +1912,7 @@ static void* output_ptr(hk_ctx* c, int id, uint32_t* w, uint32_t* h, uint32_t* b
     case HK_OUT_DENOISED_DIRECT: case HK_OUT_DENOISED_EMISSIVE: case HK_OUT_DENOISED_INDIRECT:
         p = c->denoised[id - HK_OUT_DENOISED_DIRECT]; break;
     case HK_OUT_TONE_MAPPED: p = c->tone_buf[c->head]; break;
+    case HK_OUT_TONE_MAPPED_PREVIOUS: p = c->tone_buf[c->head ^ 1u]; break;
     case HK_OUT_UPSCALED: p = c->upscale; W = c->upscale_wh[0]; H = c->upscale_wh[1]; break;
     case HK_OUT_TAA: p = c->taa_buf[c->head]; W = c->taa_wh[0]; H = c->taa_wh[1]; break;
     case HK_OUT_ACCUMULATED: p = c->accum_out; break;
@@ -2004,7 +2005,7 @@ int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* d
     HK_TRY(gb_join(c, st));
     if (foreign) {
         const bool from_tail = c->rf_swapped && c->tail_open &&
-                               (id == HK_OUT_TONE_MAPPED || id == HK_OUT_ACCUMULATED ||
+                               (id == HK_OUT_TONE_MAPPED || id == HK_OUT_TONE_MAPPED_PREVIOUS || id == HK_OUT_ACCUMULATED ||
                                 (id >= HK_OUT_DENOISED_DIRECT && id <= HK_OUT_DENOISED_INDIRECT));
         if (!from_tail) {
             HK_HIP(c, hipEventRecord(c->ev_frame_mark, c->frame_st));

@@ -32,6 +32,7 @@ OUT_GBUF_VELOCITY_UV = 15
 OUT_ACCUMULATED = 17
 OUT_UPSCALED = 18
 OUT_TAA = 19
+OUT_TONE_MAPPED_PREVIOUS = 20
 OUT_DENOISE_INTERNAL_VARIANCE = 16
 RESERVOIR_BUFFERS = 10
 

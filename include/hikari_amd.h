@@ -169,7 +169,9 @@ typedef enum hk_output_id {
     HK_OUT_ACCUMULATED = 17,      /* RGBA16F, s: hk_resolve_accumulation */
     HK_OUT_UPSCALED = 18,         /* RGBA16F, ceil(S * 2 / ratio): SMAA TU4x output (upscale_output[0]) */
     HK_OUT_TAA = 19,              /* RGBA16F: TAA Jasmine output of this frame (taa_output[head]) */
-    HK_OUT_COUNT = 20
+    HK_OUT_TONE_MAPPED_PREVIOUS = 20, /* RGBA16F, s: the previous frame's tone-mapped output (tone_mapping_output
+                                       * [1 - head]), intact until this frame's successor's tone-sum */
+    HK_OUT_COUNT = 21
 } hk_output_id;
 
 /* Reservoir buffer ids 0..9 as allocated by light.rs:350-361; the channel pairs
@@ -215,9 +217,10 @@ void hk_settings_default(hk_settings* out);
  *   lds_scene (1)            0 no LDS scene staging, 1 where measured faster, 2 every traversal kernel
  *   gbuffer_stack_full (0), gbuffer_deep (0), direct_w4_min_px (4e5), fused_w4 (1),
  *   persistent_indirect (0)  kernel-variant choices (tests force each variant with them)
- *   compact_emitter (1)      the fused direct/emissive launch runs a workgroup's emitter BLAS walks as one
+ *   compact_emitter (0)      the fused direct/emissive launch runs a workgroup's emitter BLAS walks as one
  *                            compacted batch (long walks first) on frames without emissive validation
  *   compact_shadow (0)       shadow walks of a workgroup as one compacted batch (fused launch, indirect pass)
+ *                            (both measured slower than the per-pixel walks: DESIGN §4)
  * hk_set_option returns HK_ERR_INVALID for an unknown key or a value outside the key's range. */
 int hk_set_option(hk_ctx* ctx, const char* key, double value);
 int hk_get_option(const hk_ctx* ctx, const char* key, double* value);

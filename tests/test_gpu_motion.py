@@ -104,8 +104,9 @@ def test_moving_camera_1080p_bit_exact():
     """The bench's moving-camera workload at full size (bench.py cornell-1080p-nee-orbit: cornell
     1920x1080, traversal + NEE, the examples' orbit camera at 0.5 deg/frame, examples.orbit): 3 frames,
     every plane bit-exact, the spatial-pair scatter targets within the stated tolerance.  With motion
-    the fused direct/emissive launch and background store elision are off: this covers the separate
-    launches at bench size."""
+    the fused direct/emissive launch is off and the direct pair's background stores are kept, while the
+    passes' own background targets and the indirect pair still elide (the direct pair bit off, the indirect
+    pair bit kept): this covers the separate launches and motion-time elision at bench size."""
     from hikari_amd import HikariSettings, Taa, Upscale, examples, frame_inputs
     w, h = 1920, 1080
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, taa=Taa.None_, indirect_spatial_reuse=False, denoise=False)
@@ -328,8 +329,9 @@ def test_background_elision_bit_exact(hk_options, launch):
     """Background store elision (ChannelArgs::bg, hk_kernels.hip bg_elide): the direct / emissive
     launches (fused, or separate sharing one mask) and the indirect pass skip a background pixel's constant zero stores once
     every target buffer holds them.  A sequence that exercises every way the mask can go stale:
-    static frames (elision active from the third frame), camera motion (separate launches: the
-    mask is dropped), static again (rebuilt), and a reservoir upload over the spatial pairs,
+    static frames (elision active from the third frame), camera motion (separate launches: each pass's
+    own background targets keep eliding, the direct pair's bit is cleared and its stores resume, the
+    indirect pair's bit stays), static again (the pair bit rebuilt), and a reservoir upload over the spatial pairs,
     after which the next frame must store the background records again.  Every plane and all 10
     reservoir buffers bit-exact against the oracle (which never elides) on every frame."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs

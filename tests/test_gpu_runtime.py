@@ -215,3 +215,39 @@ def test_band_with_host_planes_under_motion_runs_whole_band():
             a, z = (canon_plane(oid, b.output(oid)[core0:core0 + core_rows]) for b in bands)
             m = mismatch_report(a, z, f"frame {f} output {oid}: row windows vs whole band")
             assert not m, m
+
+
+@pytest.mark.parametrize("scene_fn", ["cornell", "city"])
+def test_gbuffer_stack_bound_after_instance_updates(scene_fn):
+    """The shallow G-buffer walk takes exactly the scene's stack bound (TLAS + BLAS inner levels) of LDS
+    levels, a bound the runtime recomputes from the device TLAS after every hk_update_instances (ADVICE r03:
+    an undercount would push past the workgroup's LDS).  After several GPU rebuilds with seeded transforms,
+    the G-buffer planes of the default walk equal those of the same walk with all 16 LDS levels
+    (gbuffer_stack_full) and of the deep variant with its scratch stack (gbuffer_deep), and the oracle's."""
+    from hikari_amd import HikariRenderer, examples, frame_inputs, load_noise
+    from oracle import Oracle
+    from test_gpu_parity import _moved
+    w, h = 128, 72
+    scene, cam, lights = examples.SCENES[scene_fn]()
+    ctx = []
+    for opts in ({}, {"gbuffer_stack_full": 1}, {"gbuffer_deep": 1}):
+        r = HikariRenderer(0, options=opts)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.resize(w, h, 1.0)
+        ctx.append(r)
+    for f, seed in enumerate((3, 11, 19)):
+        moved, _, _ = _moved(scene_fn, seed)
+        for r in ctx:
+            r.update_instances(moved.instance_models(), moved.instance_local_aabbs())
+            r.render_gbuffer(frame_inputs(f, cam, lights, w, h))
+        o = Oracle(moved.build(), load_noise(), w, h, 1.0)
+        o.render_gbuffer(frame_inputs(f, cam, lights, w, h))
+        for oid in (0, 11, 12, 13, 14):  # albedo, position, normal, depth gradient, ids (velocity: see motion tests)
+            planes = [canon_plane(oid, r.output(oid)) for r in ctx]
+            for k in (1, 2):
+                m = mismatch_report(planes[0], planes[k], f"update {f} output {oid}: default vs variant {k}")
+                assert not m, m
+            if oid != 0:  # (the oracle computes full_screen_albedo in its frame pass, not with the G-buffer)
+                m = mismatch_report(planes[0], canon_plane(oid, o.output(oid)), f"update {f} output {oid} vs oracle")
+                assert not m, m
