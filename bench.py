@@ -39,8 +39,8 @@ import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Taa, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, halo_rows, rebalance,  # noqa: E402
-                              stripe_gather_rows, use_stripes)
+from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, halo_rows, reassembly_copies,  # noqa: E402
+                              rebalance, stripe_gather_rows, use_stripes)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -299,12 +299,12 @@ def main():
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
     elif dist_on:
-        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 2) of a short
+        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 3) of a short
         # calibration on the current bands — frames 0..5 rendered, 3..5 timed per rank, the times all-gathered
         # — each moving the boundaries to equal measured cost.  Then every rank starts the run from frame 0
         # on its final band (hk_resize zero-fills the reservoirs, as at the start of any run).
         bounds = equal_bounds(world, H)
-        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "2")) if world > 1 else 0):
+        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "3")) if world > 1 else 0):
             b = band_of(rank, world, H, bounds)
             r.resize(W, H, 1.0, b.y0, b.rows)
             for f in range(6):
@@ -334,7 +334,8 @@ def main():
         r.resize(W, H, 1.0)
     row0, rows, core0, core_rows = r.band_info()
     # the gathered rows back in frame order (stripes; uneven bands) on a side stream after each gather
-    reorder = stripes or (bounds is not None and list(bounds) != equal_bounds(world, H))
+    # (nothing to put back when the gathered rows are already in frame order: one rank, equal bands)
+    reorder = dist_on and not np.array_equal(gather_index, np.arange(H)) if (stripes or bounds is not None) else False
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
@@ -351,6 +352,11 @@ def main():
     if reorder:  # stripes / uneven bands back in frame order, on a side stream after each gather
         frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
         index_t = torch.from_numpy(gather_index).to("cuda")
+
+        # one strided row copy per rank (bands.reassembly_copies); torch.index_select over the frame's row
+        # indices took ~0.1 ms per 1080p frame (per-element index arithmetic), the row copies a few microseconds
+        row_copies = [reassembly_copies(frame_t[k], full_t[k], world, H, band, None if stripes else bounds)
+                      for k in range(2)] if H % 8 == 0 else None
         side = torch.cuda.Stream()
         reorder_done = [None, None]
 
@@ -407,9 +413,14 @@ def main():
                 gather(f - 1, hikari_amd._abi.OUT_TONE_MAPPED_PREVIOUS)
 
     gathered = [-1]  # the latest frame whose rows were gathered
+    # HK_BENCH_COMM (diagnostic of the collective path's cost, never a result): "copy" = the band copy only,
+    # "noreorder" = copy + all-gather without the frame-order reorder, "none" = nothing
+    comm_mode = os.environ.get("HK_BENCH_COMM", "full")
 
     def gather(f, plane):
         gathered[0] = f
+        if comm_mode == "none":
+            return
         k = f & 1
         with torch.cuda.stream(comm):
             if pending[k] is not None:
@@ -417,19 +428,25 @@ def main():
             if reorder and reorder_done[k] is not None:
                 comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
             r.copy_output_rows(plane, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
+            if comm_mode == "copy":
+                return
             if rehearsal:
                 parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
                 dist.all_gather(parts, band_t[k].cpu())
                 full_t[k].copy_(torch.cat(parts))
             else:
                 pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
-        if reorder:
+        if reorder and comm_mode != "noreorder":
             with torch.cuda.stream(side):
                 if pending[k] is not None:
                     pending[k].wait()
                 else:
                     side.wait_stream(comm)
-                torch.index_select(full_t[k], 0, index_t, out=frame_t[k])
+                if row_copies is not None:
+                    for dst, src in row_copies[k]:
+                        dst.copy_(src)
+                else:
+                    torch.index_select(full_t[k], 0, index_t, out=frame_t[k])
                 reorder_done[k] = side.record_event()
 
     def drain(last):

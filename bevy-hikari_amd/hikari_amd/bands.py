@@ -122,3 +122,23 @@ def stripe_gather_rows(world: int, height: int) -> tuple:
 def use_stripes(spatial_reuse: bool, denoise: bool) -> bool:
     """Stripes where no pass reads neighbours; contiguous bands + halo otherwise."""
     return halo_rows(spatial_reuse, denoise) == 0
+
+
+def reassembly_copies(frame, gathered, world: int, height: int, pad: int, bounds=None) -> list:
+    """(destination, source) views that put an all-gather of `world` ranks x `pad` rows back in frame order:
+    one strided copy per rank moving whole rows — its interleaved 8-row stripes (bounds None) or its band of
+    `bounds`.  frame: (height, W, C), gathered: (world * pad, W, C) tensors (torch or numpy, with .view /
+    .reshape on contiguous buffers); height must be a multiple of STRIPE_H for stripes."""
+    out = []
+    for q in range(world):
+        if bounds is None:
+            if height % STRIPE_H:
+                raise ValueError("stripe reassembly needs a height that is a multiple of 8")
+            n = len(stripe_rows(q, world, height)) // STRIPE_H
+            dst = frame.view(height // STRIPE_H, STRIPE_H, *frame.shape[1:])[q::world][:n]
+            src = gathered[q * pad: q * pad + n * STRIPE_H].view(n, STRIPE_H, *frame.shape[1:])
+        else:
+            b = band_of(q, world, height, bounds)
+            dst, src = frame[b.y0: b.y0 + b.rows], gathered[q * pad: q * pad + b.rows]
+        out.append((dst, src))
+    return out

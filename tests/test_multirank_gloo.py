@@ -248,3 +248,28 @@ def test_rebalance_converges_on_a_skewed_cost():
             assert b[0] == 0 and b[-1] == height and all(np.diff(b) >= BAND_ALIGN)
             assert all(v % BAND_ALIGN == 0 for v in b)
         assert first > 1.3 and t.max() / t.mean() < 1.06, (world, first, t.max() / t.mean())
+
+
+@pytest.mark.parametrize("world,height", [(2, 192), (8, 1080), (8, 2160), (3, 256)])
+def test_reassembly_row_copies_equal_the_gather_index(world, height):
+    """bench.py puts the all-gathered stripes / uneven bands back in frame order with one strided row copy
+    per rank (bands.reassembly_copies); the result equals the gather index's reordering for both layouts."""
+    import torch
+
+    from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, reassembly_copies, rebalance,
+                                  stripe_gather_rows, stripe_rows)
+    w = 5
+    frame = torch.arange(height * w * 4, dtype=torch.float32).view(height, w, 4)
+    for bounds in (None, rebalance(equal_bounds(world, height), np.arange(1, world + 1, dtype=float))):
+        pad, index = stripe_gather_rows(world, height) if bounds is None else band_gather_rows(bounds)
+        gathered = torch.zeros(world * pad, w, 4)
+        for q in range(world):
+            rows = stripe_rows(q, world, height) if bounds is None else \
+                np.arange(band_of(q, world, height, bounds).y0, band_of(q, world, height, bounds).y0 +
+                          band_of(q, world, height, bounds).rows)
+            gathered[q * pad: q * pad + len(rows)] = frame[torch.from_numpy(np.asarray(rows))]
+        out = torch.full_like(frame, -1.0)
+        for dst, src in reassembly_copies(out, gathered, world, height, pad, bounds):
+            dst.copy_(src)
+        assert torch.equal(out, frame)
+        assert torch.equal(gathered[torch.from_numpy(index)], frame)
