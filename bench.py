@@ -583,7 +583,8 @@ def main():
                        "rays_per_frame": int(rays // (args.steps * spp)),
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
-                                       f"cost-balanced row-bands x{world} + RCCL all-gather") if world > 1 else "single GPU",
+                                       f"cost-balanced row-bands x{world} + RCCL all-gather") if world > 1 else
+                                      ("single GPU through the RCCL path (world size 1)" if dist_on else "single GPU"),
                        "band_bounds": None if bounds is None else [int(v) for v in bounds],
                        "band_calibration": balance or None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -646,12 +646,15 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
 //   L3, L2, L1, L0 run on core +-0, 1, 3, 7 rows and demodulation on +-15; its 3x3 variance blur
 //   (denoise.wgsl:151-159) reads the light passes' render / variance at +-16 (OUT);
 //   spatial reuse runs on core +-OUT and reads the temporal reservoirs and the G-buffer depth
-//   within its RANGE (20 px indirect, 10 emissive: light.wgsl:1568-1600), so the temporal
-//   passes and the G-buffer run on core +-(OUT + RANGE).
+//   within its RANGE (20 px indirect, 10 emissive: light.wgsl:1568-1600), so each channel's temporal
+//   pass runs on core +-(OUT + its RANGE) — direct_lit has no spatial pass (light.rs:656-676), so the
+//   direct / emissive launch needs only +-OUT when emissive spatial reuse is off — and the G-buffer on
+//   core +-(OUT + 20).
 // For a static camera every other read is the pixel's own (temporal reprojection is the
 // identity), so the core rows stay bit-identical to the whole frame (test_gpu_row_bands_*),
 // with 1.15x instead of 1.30x the work of an 8-way city 4K band.  Rows outside a pass's window
-// keep stale values that no windowed pass reads.  Option band_full_windows: every pass on all rows.
+// keep stale values that no windowed pass reads (a settings change that widens a window later reads
+// them: band outputs are exact for a fixed setting).  Option band_full_windows: every pass on all rows.
 constexpr int32_t DENOISE_OUT_REACH = 16, SPATIAL_RANGE = 20, EMISSIVE_SPATIAL_RANGE = 10;
 constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
 // Only for a static frame: under camera or instance motion temporal reprojection reads the previous
@@ -1599,8 +1602,11 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         const FrameArgs AG = pass_window(c, A_all, GBUFFER_REACH);
         timed(c, "full_screen_albedo", st, [&] { launch_albedo(AG, c->albedo, st); });
     }
-    // per-pass row windows of a band (pass_window): temporal passes, then spatial reuse
-    A = pass_window(c, A_all, light_out_reach(settings) + spatial_range(settings));
+    // per-pass row windows of a band (pass_window): each channel's temporal pass on the rows its spatial
+    // pass reads (core +-(OUT + that channel's range): direct_lit has no spatial pass, light.rs:656-676),
+    // then spatial reuse.  A: the indirect channel; AE: direct + emissive.
+    A = pass_window(c, A_all, light_out_reach(settings) + (settings->indirect_spatial_reuse ? SPATIAL_RANGE : 0));
+    FrameArgs AE = pass_window(c, A_all, light_out_reach(settings) + (settings->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0));
     const FrameArgs AS = pass_window(c, A_all, light_out_reach(settings));
     ChannelArgs C0 = channel(c, A.F.number, 0);
     ChannelArgs C1 = channel(c, A.F.number, 1);
@@ -1648,6 +1654,8 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     const bool merge_possible = identity && fork && !multi && !wf && !light_lds_direct(A) && c->on(OPT_FUSE);
     const bool merge_default = !pipeline_size(c) && !settings->indirect_spatial_reuse && !settings->emissive_spatial_reuse;
     const bool merge = merge_possible && (c->opt[OPT_MERGE] < 0.0 ? merge_default : c->on(OPT_MERGE));
+    // (one grid for all three channels: the wider window)
+    if (merge) A = AE = pass_window(c, A_all, light_out_reach(settings) + spatial_range(settings));
     if (fork && !merge) {
         if (gb_fresh && c->rf_side_only && swap && c->albedo_fresh && !had_ext) {
             // The fork marker would make the side stream wait for the caller stream here.  What the
@@ -1667,7 +1675,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
         }
         fork_events = true;
     }
-    HK_TRY(bg_mask(c, 0, A, elide, identity && !settings->emissive_spatial_reuse, st, C0));
+    HK_TRY(bg_mask(c, 0, AE, elide, identity && !settings->emissive_spatial_reuse, st, C0));
     C1.bg = C0.bg;
     C1.bg_need = C0.bg_need;
     if (merge) {
@@ -1680,10 +1688,10 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
             timed(c, "indirect_spatial_reuse", st, [&] { launch_spatial(AS, C2, false, st); });
     } else {
         if (fuse) {
-            timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(A, C0, C1, st); });
+            timed(c, "direct_lit_emissive", st, [&] { launch_direct_fused(AE, C0, C1, st); });
         } else {
-            timed(c, "direct_lit", st, [&] { launch_direct(A, C0, false, st); });
-            timed(c, "direct_emissive", s1, [&] { launch_direct(A, C1, true, s1); });
+            timed(c, "direct_lit", st, [&] { launch_direct(AE, C0, false, st); });
+            timed(c, "direct_emissive", s1, [&] { launch_direct(AE, C1, true, s1); });
         }
         if (settings->emissive_spatial_reuse) timed(c, "emissive_spatial_reuse", s1, [&] { launch_spatial(AS, C1, true, s1); });
         // (the wavefront pass elides in its generation stage, which classifies every pixel)

@@ -258,21 +258,23 @@ def test_trace_matches_oracle():
 
 
 @pytest.mark.parametrize("spatial,denoise,world,H", [(True, True, 2, 96), (False, False, 2, 96), (True, True, 4, 192),
-                                                     (True, False, 3, 192), (False, True, 3, 192)])
+                                                     (True, False, 3, 192), (False, True, 3, 192),
+                                                     ("indirect", True, 3, 192)])
 def test_gpu_row_bands_match_whole_frame(spatial, denoise, world, H):
     """Band contexts (the multi-GPU decomposition, run on one GPU) reproduce the whole-frame
     oracle render bit-exactly on their own rows, and count only their own rays.  At H = 192 the
     bands' halos and the per-pass row windows (hk_runtime.hip pass_window: G-buffer and temporal
     passes on core +-36, spatial reuse +-16, demodulation +-15, the a-trous levels +-7/3/1/0) are
-    strict parts of the frame, over 5 frames of reservoir history."""
+    strict parts of the frame, over 5 frames of reservoir history.  spatial = "indirect": indirect
+    spatial reuse alone (the bench configs), where the direct / emissive launch runs on core +-16 only."""
     from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
     from hikari_amd.bands import band_of, halo_rows
     from oracle import Oracle
     W = 64
     scene, cam, lights = examples.cornell()
     desc = scene.build()
-    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=spatial, emissive_spatial_reuse=spatial,
-                        denoise=denoise)
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=bool(spatial),
+                        emissive_spatial_reuse=spatial is True, denoise=denoise)
     s = st.to_c()
     o = Oracle(desc, load_noise(), W, H, 1.0)
     ranks = []
@@ -281,7 +283,7 @@ def test_gpu_row_bands_match_whole_frame(spatial, denoise, world, H):
         r = HikariRenderer(0)
         r.set_noise()
         r.upload_scene(scene)
-        r.set_band_halo(halo_rows(spatial, denoise))
+        r.set_band_halo(halo_rows(bool(spatial), denoise))
         r.resize(W, H, 1.0, b.y0, b.rows)
         ranks.append((b, r))
     for f in range(5):
