@@ -585,6 +585,57 @@ HKD bool check_previous_reservoir(Reservoir& r, const Sample& s)
     }
     return true;
 }
+// load_previous + check_previous_reservoir read in two steps (the light passes' register peaks): the record's
+// index and the words the check reads — chunk 3 (count, weights, visible normal, lifetime), the depth word of
+// chunk 1 and the instance word of chunk 2 — first; the whole record later, with previous_record(), where the pass
+// needs its sample.  The passes do not write their previous temporal buffer, so the second read returns the same
+// bits: previous_record(previous_head(F, b, uv, s)) == the reservoir check_previous_reservoir leaves in
+// load_previous(F, b, uv), and `kept` is its result.
+struct PrevHead {
+    int32_t index;  // load_previous's record; -1: outside the frame (the zero reservoir, which the check rejects)
+    bool kept;      // check_previous_reservoir passed (otherwise the reservoir is the zero reservoir)
+    float count, lifetime, w_sum, w2_sum;
+};
+HKD PrevHead previous_head(const Frame& F, const ResBuf& b, f2 uv, const Sample& s)
+{
+    PrevHead h;
+    h.index = -1;
+    h.kept = false;
+    h.count = h.lifetime = h.w_sum = h.w2_sum = 0.0f;
+    if (uv_inside_open(uv)) h.index = s_index(F, f2i32(uv.x * (float)F.s[0]), f2i32(uv.y * (float)F.s[1]));
+    if (h.index >= 0) {
+        const uint32_t u = (uint32_t)h.index;
+        const uint4 c3 = b.base[res_chunk(b, 3u, u)];
+        const float depth = __uint_as_float(b.base[res_chunk(b, 1u, u)].w);
+        const uint32_t instance = f2u32(__uint_as_float(b.base[res_chunk(b, 2u, u)].w));
+        const f3 normal = normalize(mk3(hk_unpack_snorm8_fast(c3.x, 0), hk_unpack_snorm8_fast(c3.x, 1), hk_unpack_snorm8_fast(c3.x, 2)));
+        // check_previous_reservoir on the decoded fields
+        float depth_ratio = depth / s.visible_position.w;
+        depth_ratio = depth_ratio < 1.0f ? 1.0f / depth_ratio : depth_ratio;
+        const bool depth_miss = depth_ratio > 1.05f * (1.0f + 0.5f * s.random.x);
+        const bool instance_miss = instance != s.visible_instance;
+        const bool normal_miss = dot(s.visible_normal, normal) < 0.9f;
+        h.kept = !(depth_miss || normal_miss || instance_miss);
+        if (h.kept) {
+            h.count = unpack_lo16float(c3.z);
+            h.w_sum = unpack_lo16float(c3.w);
+            h.w2_sum = unpack_hi16float(c3.w);
+            h.lifetime = 127.0f * (1.0f + hk_unpack_snorm8_fast(c3.x, 3));
+        }
+    }
+    return h;
+}
+HKD Reservoir previous_record(const ResBuf& b, const PrevHead& h)
+{
+    return h.kept ? load_res(b, h.index) : zero_reservoir();
+}
+// the scatter of a rejected previous reservoir (light.wgsl:1092-1095, 1453-1457): the zero reservoir, at the
+// previous uv's pixel when that uv is inside the frame
+HKD void scatter_rejected(const Frame& F, const ResBuf& prev_spatial, f2 uv, const PrevHead& h)
+{
+    if (!h.kept && uv_inside_closed(uv))
+        store_res(prev_spatial, s_index(F, f2i32(uv.x * (float)F.s[0]), f2i32(uv.y * (float)F.s[1])), zero_reservoir());
+}
 HKD void temporal_restir(Reservoir& r, const Sample& s, float w_new, uint32_t max_sample_count)
 {
     update_reservoir(r, s, w_new);
@@ -689,7 +740,10 @@ HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& 
 // the flattened array, bvh flatten).  All STEPS nodes are loaded and tested up front with the
 // same hit distance (no leaf work happens between such visits).  Returns the node the walk visits
 // next; `leaf_pass`/`leaf_entry` report the leaf reached in this iteration, if its box passed.
-constexpr int WALK_STEPS = 2;  // visits per walk iteration (3 and 4 measured slower)
+#ifndef HK_WALK_STEPS
+#define HK_WALK_STEPS 2
+#endif
+constexpr int WALK_STEPS = HK_WALK_STEPS;  // visits per walk iteration (3 and 4 measured slower)
 template <int STEPS>
 HKD uint32_t walk_step(const hk_node* nodes, uint32_t index, uint32_t count, const Ray& tr, float distance,
                        bool& leaf_pass, uint32_t& leaf_entry)

@@ -462,6 +462,10 @@ HKD bool direct_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& C,
 
     f2 juv = jittered_uv(F, uv, 0.25f);
     D.previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
+    // (the whole previous record is read here, before the walks, which hide its latency: read in two steps as in
+    // k_indirect's tail — previous_head before the walks, previous_record after them — the fused kernel needs 97
+    // instead of 113 VGPRs but the second read lands on the critical path: cornell 0.181 -> 0.194 ms, city 4K
+    // 1.337 -> 1.432 ms, profiles/r04/c9)
     Reservoir& r = D.r;
     r = load_previous(F, C.prev, D.previous_uv);
     if (!check_previous_reservoir(r, s) && uv_inside_closed(D.previous_uv)) {
@@ -1305,36 +1309,9 @@ HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C,
     // reservoir, without the previous sample's registers live next to the new sample's shading.
     f2 juv = jittered_uv(F, uv, 0.25f);
     f2 previous_uv = mk2(juv.x - velocity_uv.x, juv.y - velocity_uv.y);
-    int32_t pidx = -1;  // load_previous's record; -1: outside the frame (the zero reservoir, which the check rejects)
-    if (uv_inside_open(previous_uv))
-        pidx = s_index(F, f2i32(previous_uv.x * (float)F.s[0]), f2i32(previous_uv.y * (float)F.s[1]));
-    float r_count = 0.0f, r_lifetime = 0.0f, r_w_sum = 0.0f, r_w2_sum = 0.0f;
-    bool kept = false;  // check_previous_reservoir passed
-    if (pidx >= 0) {
-        const uint32_t u = (uint32_t)pidx;
-        const uint4 c3 = C.prev.base[res_chunk(C.prev, 3u, u)];
-        const float p_depth = __uint_as_float(C.prev.base[res_chunk(C.prev, 1u, u)].w);
-        const uint32_t p_instance = f2u32(__uint_as_float(C.prev.base[res_chunk(C.prev, 2u, u)].w));
-        const f3 p_normal = normalize(mk3(hk_unpack_snorm8_fast(c3.x, 0), hk_unpack_snorm8_fast(c3.x, 1), hk_unpack_snorm8_fast(c3.x, 2)));
-        // check_previous_reservoir (hk_device.h), on the decoded fields
-        float depth_ratio = p_depth / s.visible_position.w;
-        depth_ratio = depth_ratio < 1.0f ? 1.0f / depth_ratio : depth_ratio;
-        const bool depth_miss = depth_ratio > 1.05f * (1.0f + 0.5f * s.random.x);
-        const bool instance_miss = p_instance != s.visible_instance;
-        const bool normal_miss = dot(s.visible_normal, p_normal) < 0.9f;
-        kept = !(depth_miss || normal_miss || instance_miss);
-        if (kept) {
-            r_count = unpack_lo16float(c3.z);
-            r_w_sum = unpack_lo16float(c3.w);
-            r_w2_sum = unpack_hi16float(c3.w);
-            r_lifetime = 127.0f * (1.0f + hk_unpack_snorm8_fast(c3.x, 3));
-        }
-    }
-    if (!kept && uv_inside_closed(previous_uv)) {
-        int32_t px = f2i32(previous_uv.x * (float)F.s[0]);
-        int32_t py = f2i32(previous_uv.y * (float)F.s[1]);
-        store_res(C.prev_spatial, s_index(F, px, py), zero_reservoir());
-    }
+    const PrevHead ph = previous_head(F, C.prev, previous_uv, s);
+    scatter_rejected(F, C.prev_spatial, previous_uv, ph);
+    float r_count = ph.count, r_lifetime = ph.lifetime, r_w_sum = ph.w_sum, r_w2_sum = ph.w2_sum;
     surface = retreive_surface(sc, im_y, mk2(velocity_uv.z, velocity_uv.w));
     f3 view_direction = calculate_view(F, position);
     f3 sample_radiance = shading(F, view_direction, s.visible_normal,
@@ -1354,8 +1331,7 @@ HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C,
         }
     }
     if (take) r.s = s;
-    else if (kept) r.s = load_res(C.prev, pidx).s;
-    else r.s = zero_sample();
+    else r.s = previous_record(C.prev, ph).s;
     r.count = r_count;
     r.lifetime = r_lifetime;
     r.w_sum = r_w_sum;
