@@ -56,17 +56,33 @@ HKD f3 mix(f3 a, f3 b, float t)
 // test_fast_reciprocal_is_exact): v_rcp_f32 (within 1 ulp) plus FMA residual corrections where
 // neither d nor 1/d is near the denormal range; the IEEE divide sequence elsewhere (0, inf, NaN,
 // |d| outside [2^-125, 2^125]).  Half the instructions of the divide.
-HKD float rcp_exact(float d)
+// The corrected estimate is computed unconditionally and the divide only behind a branch that waves skip when
+// none of their lanes needs it (one exec-mask region instead of an if / else pair).
+HKD bool rcp_fast_ok(float d)
 {
     const float a = fabsf(d);
-    if (a >= 0x1p-125f && a <= 0x1p125f) {
-        float r = __builtin_amdgcn_rcpf(d);
-        r = fmaf(fmaf(-d, r, 1.0f), r, r);
-        return r;
-    }
-    return 1.0f / d;
+    return a >= 0x1p-125f && a <= 0x1p125f;
 }
-HKD f3 inv(f3 d) { return mk3(rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)); }
+HKD float rcp_fast(float d)
+{
+    const float r = __builtin_amdgcn_rcpf(d);
+    return fmaf(fmaf(-d, r, 1.0f), r, r);
+}
+HKD float rcp_exact(float d)
+{
+    float r = rcp_fast(d);
+    if (__builtin_expect(!rcp_fast_ok(d), 0)) r = 1.0f / d;
+    return r;
+}
+// three reciprocals with one rare-path branch: where the fast result is exact it equals the IEEE quotient, so the
+// branch may divide all three components
+HKD f3 inv(f3 d)
+{
+    f3 r = mk3(rcp_fast(d.x), rcp_fast(d.y), rcp_fast(d.z));
+    const bool ok = (int)rcp_fast_ok(d.x) & (int)rcp_fast_ok(d.y) & (int)rcp_fast_ok(d.z);
+    if (__builtin_expect(!ok, 0)) r = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    return r;
+}
 HKD f3 normalize(f3 a) { return a * rcp_exact(sqrtf(dot(a, a))); }
 HKD float sum4(f4 a) { return ((a.x + a.y) + a.z) + a.w; }
 HKD float lum(f3 c) { return hk_luminance(c.x, c.y, c.z); }
@@ -693,26 +709,25 @@ HKD float intersects_aabb(const Ray& ray, f3 mn, f3 mx)
 }
 
 // Möller–Trumbore as light.wgsl:364-398; returns distance (F32_MAX on miss) and uv.
+// Written without early returns: every value is computed and the result selected at the end (the values of the
+// reference's early exits are the selects' other arms), so a wave whose lanes leave at different tests runs one
+// straight sequence instead of three exec-mask regions.
 HKD float intersects_triangle(const Ray& ray, f3 p0, f3 p1, f3 p2, f2& uv_out)
 {
-    uv_out = mk2(0.0f, 0.0f);
     f3 ab = p1 - p0;
     f3 ac = p2 - p0;
     f3 u_vec = cross(ray.direction, ac);
     float det = dot(ab, u_vec);
-    if (fabsf(det) < HK_F32_EPSILON) return HK_F32_MAX;
+    const bool parallel = fabsf(det) < HK_F32_EPSILON;
     float inv_det = rcp_exact(det);
     f3 ao = ray.origin - p0;
     float u = dot(ao, u_vec) * inv_det;
-    if (u < 0.0f || u > 1.0f) {
-        uv_out = mk2(u, 0.0f);
-        return HK_F32_MAX;
-    }
+    const bool u_miss = u < 0.0f || u > 1.0f;
     f3 v_vec = cross(ao, ab);
     float v = dot(ray.direction, v_vec) * inv_det;
-    uv_out = mk2(u, v);
-    if (v < 0.0f || u + v > 1.0f) return HK_F32_MAX;
     float distance = dot(ac, v_vec) * inv_det;
+    uv_out = parallel ? mk2(0.0f, 0.0f) : mk2(u, u_miss ? 0.0f : v);
+    if (parallel || u_miss || v < 0.0f || u + v > 1.0f) return HK_F32_MAX;
     return distance > HK_F32_EPSILON ? distance : HK_F32_MAX;
 }
 
