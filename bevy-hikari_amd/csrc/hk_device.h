@@ -914,6 +914,7 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
     hit.distance = max_distance;
     hit.instance_index = HK_U32_MAX;
     hit.primitive_index = HK_U32_MAX;
+#if HK_WALK_SELECT
     uint32_t top = 0u;                  // next TLAS node
     uint32_t bot = 0u, bot_count = 0u;  // BLAS walk state (in_bottom: inside an instance)
     uint32_t bot_base = 0u, prim_offset = 0u, cur_instance = 0u;
@@ -978,6 +979,75 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
         }
     }
     return hit;
+#else
+    // The walk in progress — the TLAS, or the BLAS of the instance being visited — as one set of registers (its
+    // nodes, length, position and ray), switched when the walk enters or leaves an instance, so that an iteration
+    // selects nothing between the two levels' states.
+    const hk_node* nodes = sc.instance_nodes;
+    uint32_t count = sc.n_instance_nodes, index = 0u;
+    Ray tr = ray;                       // the current walk's ray (the instance-local ray inside a BLAS)
+    uint32_t top = 0u;                  // the TLAS walk's next node while a BLAS is walked
+    uint32_t prim_offset = 0u, cur_instance = 0u;
+    bool in_bottom = false, intersected = false;
+    HK_LANE_STATS_DECL;
+    while (index < count) {
+        HK_LANE_STATS_TICK;
+        // BLAS leaves carry their triangle's box (k_fill_blas_leaves, light.wgsl:411-413), TLAS
+        // leaves their instance's min/max (k_fill_tlas_leaves, light.wgsl:456-457); the leaf this
+        // iteration reaches (if any) and the node after it
+        bool leaf_pass;
+        uint32_t leaf_entry;
+        index = walk_step<WALK_STEPS>(nodes, index, count, tr, hit.distance, leaf_pass, leaf_entry);
+        if (in_bottom) {
+            bool stop = false;
+            if (leaf_pass) {
+                const uint32_t primitive_index = prim_offset + leaf_entry - HK_BVH_LEAF_FLAG;
+                f3 a, b, c;
+                load_triangle(sc.primitives, primitive_index, a, b, c);
+                f2 uv;
+                const float d = intersects_triangle(tr, a, b, c, uv);
+                if (d < hit.distance) {
+                    hit.distance = d;
+                    hit.uv = uv;
+                    hit.primitive_index = primitive_index;
+                    intersected = true;
+                    stop = d < early_distance;  // traverse_bottom's early return
+                }
+            }
+            if (stop || index >= count) {  // back in traverse_top after traverse_bottom
+                in_bottom = false;
+                nodes = sc.instance_nodes;
+                count = sc.n_instance_nodes;
+                index = top;
+                tr = ray;
+                if (intersected) {
+                    hit.instance_index = cur_instance;
+                    if (hit.distance < early_distance) return hit;
+                }
+            }
+        } else {
+            const uint32_t instance_index = leaf_entry - HK_BVH_LEAF_FLAG;
+            if (leaf_pass && instance_index != exclude) {
+                const hk_instance& in = sc.instances[instance_index];
+                const uint32_t bot_count = in.mesh.node[1];
+                prim_offset = in.mesh.primitive;
+                cur_instance = instance_index;
+                intersected = false;
+                if (bot_count > 0u) {  // traverse_bottom over an empty range does nothing
+                    in_bottom = true;
+                    top = index;
+                    nodes = sc.asset_nodes + in.mesh.node[0];
+                    count = bot_count;
+                    index = 0u;
+                    tr.origin = world_to_local_point(in, ray.origin);
+                    tr.direction = world_to_local_dir(in, ray.direction);
+                    tr.inv_direction = inv(tr.direction);
+                }
+            }
+        }
+    }
+    return hit;
+#endif
 }
 
 // ------------------------------------------------------------------ G-buffer visibility
