@@ -246,14 +246,20 @@ HKD Scene stage_scene(const Scene& g, uint32_t* lds)
         (const uint32_t*)g.materials,      (const uint32_t*)g.emissive_nodes, (const uint32_t*)g.emissives,
         (const uint32_t*)g.blas_wide,      (const uint32_t*)g.tlas_wide};
     uint32_t* dst[SCENE_ARRAYS];
-    uint32_t off = 0;
+    uint4* const lds4 = reinterpret_cast<uint4*>(lds);  // (hk_lds_scene is 16-byte aligned)
+    uint32_t off4 = 0;                                  // in 16-byte units: every array starts on a 16-byte boundary
 #pragma unroll
     for (int k = 0; k < SCENE_ARRAYS; ++k) {
-        dst[k] = lds + off;
+        uint4* const d4 = lds4 + off4;
+        dst[k] = reinterpret_cast<uint32_t*>(d4);
         if (!plan_has(PLAN, k)) continue;
         const uint32_t words = g.bytes[k] >> 2;
-        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) dst[k][i] = src[k][i];
-        off += (words + 3u) & ~3u;
+        // 16-byte copies (the sources are their own allocations), then the few trailing words
+        const uint32_t n4 = words >> 2;
+        const uint4* s4 = reinterpret_cast<const uint4*>(src[k]);
+        for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+        for (uint32_t i = (n4 << 2) + threadIdx.x; i < words; i += blockDim.x) dst[k][i] = src[k][i];
+        off4 += (words + 3u) >> 2;
     }
     __syncthreads();
     Scene s = g;

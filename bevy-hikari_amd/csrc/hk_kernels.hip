@@ -195,7 +195,7 @@ HKD f2 motion_vector(const ViewArgs& V, const hk_instance& in, uint32_t instance
     return mk2(a.x - b.x, a.y - b.y);
 }
 
-extern __shared__ uint32_t hk_lds_scene[];
+extern __shared__ __attribute__((aligned(16))) uint32_t hk_lds_scene[];  // 16-byte aligned: stage_scene copies uint4
 
 // full_screen_albedo (light.wgsl:1019-1042) of one deferred pixel from the G-buffer values as
 // they are stored (snorm8 normal, f32 position, material id and uv): k_albedo, and fused into
