@@ -247,6 +247,42 @@ HKD Scene stage_scene(const Scene& g, uint32_t* lds)
         (const uint32_t*)g.blas_wide,      (const uint32_t*)g.tlas_wide};
     uint32_t* dst[SCENE_ARRAYS];
     uint4* const lds4 = reinterpret_cast<uint4*>(lds);  // (hk_lds_scene is 16-byte aligned)
+#ifndef HK_STAGE_FLAT
+#define HK_STAGE_FLAT 1
+#endif
+#if HK_STAGE_FLAT
+    // The plan's arrays as one list of 16-byte chunks (array k at chunk off4[k], its last chunk rounded up: the
+    // bytes read past an array's end lie in the same 16-byte block of its own allocation, and no reader looks at
+    // them in LDS), copied four chunks per thread per iteration with the four loads issued before any store
+    // (cornell: 12 KiB, ~770 chunks, one iteration).
+    uint32_t off4[SCENE_ARRAYS];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < SCENE_ARRAYS; ++k) {
+        off4[k] = total;
+        dst[k] = reinterpret_cast<uint32_t*>(lds4 + total);
+        if (plan_has(PLAN, k)) total += (g.bytes[k] + 15u) >> 4;
+    }
+    if (total > 0u) {
+        for (uint32_t c0 = threadIdx.x; c0 < total; c0 += 4u * blockDim.x) {
+            uint4 v[4];
+            uint32_t cs[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t c = min(c0 + (uint32_t)j * blockDim.x, total - 1u);
+                const uint4* p = nullptr;
+#pragma unroll
+                for (int k = 0; k < SCENE_ARRAYS; ++k)
+                    if (plan_has(PLAN, k) && c >= off4[k]) p = reinterpret_cast<const uint4*>(src[k]) + (c - off4[k]);
+                v[j] = *p;
+                cs[j] = c;
+            }
+            // (unconditional: a clamped chunk is the last one, stored again with the same bits)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) lds4[cs[j]] = v[j];
+        }
+    }
+#else
     uint32_t off4 = 0;                                  // in 16-byte units: every array starts on a 16-byte boundary
 #pragma unroll
     for (int k = 0; k < SCENE_ARRAYS; ++k) {
@@ -261,6 +297,7 @@ HKD Scene stage_scene(const Scene& g, uint32_t* lds)
         for (uint32_t i = (n4 << 2) + threadIdx.x; i < words; i += blockDim.x) dst[k][i] = src[k][i];
         off4 += (words + 3u) >> 2;
     }
+#endif
     __syncthreads();
     Scene s = g;
     if (plan_has(PLAN, 0)) s.vertices = (const hk_vertex*)dst[0];
