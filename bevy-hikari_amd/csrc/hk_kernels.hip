@@ -1969,8 +1969,36 @@ __global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, Cha
         tile_origin<HK_SPATIAL_ORDER>(A.F, A.F.s_row0, x0, y0);
         W.x0 = x0 - SP_HALO;
         W.y0 = y0 - SP_HALO;
-        for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256)
-            win[k] = load_depth(A.F, A.G, W.x0 + k % SP_WIN, W.y0 + k / SP_WIN);
+        // load_depth of the 3600 window texels, 15 per thread: all 15 loads issued before any LDS store (at
+        // clamped coordinates, so none is conditional; outside the frame the value is then 0 as load_depth's),
+        // instead of one load -> wait -> store round trip per texel
+        // (the window variant runs on row bands, never on interleaved stripes: band_index is the band's row offset
+        // and clamp; texel k = t + 256 j steps 4 rows and 16 columns per j)
+        constexpr int32_t N = SP_WIN * SP_WIN, PER = (N + 255) / 256;
+        static_assert(256 / SP_WIN == 4 && 256 % SP_WIN == 16, "window stepping");
+        float v[PER];
+        int32_t col = (int32_t)threadIdx.x % SP_WIN, row = (int32_t)threadIdx.x / SP_WIN;
+        const int32_t S0 = (int32_t)A.F.S[0], S1 = (int32_t)A.F.S[1];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int32_t wx = W.x0 + col, wy = W.y0 + row;
+            const int32_t cx = min(max(wx, 0), S0 - 1), cy = min(max(wy, 0), S1 - 1);
+            int32_t ly = cy - A.F.S_row0;
+            ly = ly < 0 ? 0 : (ly >= A.F.S_rows ? A.F.S_rows - 1 : ly);
+            const float d = A.G.position[cx + S0 * ly].w;
+            v[j] = in_frame(wx, wy, A.F.S) ? d : 0.0f;
+            col += 16;
+            row += 4;
+            if (col >= SP_WIN) {
+                col -= SP_WIN;
+                row += 1;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int32_t k = (int32_t)threadIdx.x + j * 256;
+            if (j < PER - 1 || k < N) win[k] = v[j];
+        }
         if constexpr (HK_SP_P0WIN && VIEW) {
             for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256) {
                 const int32_t wx = W.x0 + k % SP_WIN, wy = W.y0 + k / SP_WIN;
