@@ -1959,7 +1959,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 }
 
 template <bool EMISSIVE_LIT, bool WINDOW, bool VIEW>
-__global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, ChannelArgs C)
+HKD void spatial_kernel(const FrameArgs& A, const ChannelArgs& C)
 {
     __shared__ float win[WINDOW ? SP_WIN * SP_WIN : 1];
     __shared__ uint4 p0win[(HK_SP_P0WIN && WINDOW && VIEW) ? SP_WIN * SP_WIN : 1];
@@ -2014,6 +2014,24 @@ __global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial(FrameArgs A, Cha
     int32_t x, y;
     if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT, WINDOW, VIEW>(A, C, x, y, W);
 }
+// The window variant (upscale ratio 1) at 6 waves per SIMD: its neighbour loop fits 78 VGPRs without spilling once
+// the window staging no longer holds 15 loads' worth of state per texel loop (city 4K 1.587 -> 1.481 ms, scene
+// 0.489 -> 0.464 ms, profiles/r04/c15; the 14.4 KiB window allows 11 workgroups per CU).  The variant without the
+// window (upscale ratio 2, host G-buffers) would spill there and keeps the compiler's choice.
+#ifndef HK_SPATIAL_WIN_WAVES
+#define HK_SPATIAL_WIN_WAVES 6
+#endif
+template <bool EMISSIVE_LIT, bool VIEW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HK_SPATIAL_WIN_WAVES, 8))) void k_spatial(FrameArgs A,
+                                                                                                             ChannelArgs C)
+{
+    spatial_kernel<EMISSIVE_LIT, true, VIEW>(A, C);
+}
+template <bool EMISSIVE_LIT, bool VIEW>
+__global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial_nowin(FrameArgs A, ChannelArgs C)
+{
+    spatial_kernel<EMISSIVE_LIT, false, VIEW>(A, C);
+}
 
 // ------------------------------------------------------------------ denoise (denoise.wgsl)
 __constant__ float KERNEL3[3][3] = {{0.0625f, 0.125f, 0.0625f}, {0.125f, 0.25f, 0.125f}, {0.0625f, 0.125f, 0.0625f}};
@@ -2052,10 +2070,23 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
     f2 duv = jittered_uv(F, uv, 0.5f);
     int32_t ax, ay, rx, ry;
     nearest_texel(duv, F.S, ax, ay);
+#if HK_DEMOD_BRANCHY
     // geometry the denoise levels read for this pixel (denoise.wgsl:220-223, 197-200)
     store_geom(D, idx, normalize(load_normal(F, A.G, ax, ay)), load_depth(F, A.G, ax, ay),
                load_instance_material(F, A.G, ax, ay).x, load_depth_gradient(F, A.G, ax, ay));
     f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
+#else
+    // (ax, ay) is a nearest_texel: inside the frame, so the load_* bounds tests always pass; the texels are read
+    // directly, without their branch regions, so all of them are in flight together (same texels, same values)
+    {
+        const int32_t g = band_index(F, ax, ay, F.S[0], F.S_row0, F.S_rows);
+        const uint32_t n = A.G.normal[g];
+        const f3 normal = mk3(hk_unpack_snorm8_fast(n, 0), hk_unpack_snorm8_fast(n, 1), hk_unpack_snorm8_fast(n, 2));
+        const float2 grad = A.G.depth_gradient[g];
+        store_geom(D, idx, normalize(normal), A.G.position[g].w, A.G.instance_material[g].x, mk2(grad.x, grad.y));
+    }
+    f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
+#endif
     nearest_texel(uv, F.s, rx, ry);
     const int32_t ridx = s_index(F, rx, ry);
 #pragma unroll
@@ -2069,12 +2100,21 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
         for (int k = 0; k < 9; ++k) {
             const int ox = k / 3 - 1, oy = k % 3 - 1;  // (-1,-1),(-1,0),(-1,1),(0,-1),...
             f2 suv = mk2(uv.x + (float)ox / (float)F.s[0], uv.y + (float)oy / (float)F.s[1]);
+#if HK_DEMOD_BRANCHY
             if (uv_outside(suv)) continue;
             int32_t vx, vy;
             nearest_texel(suv, F.s, vx, vy);
             float v = D.variance[ch][s_index(F, vx, vy)];
             if (v > HK_F32_MAX) continue;
             sum_variance += KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
+#else
+            // every tap read (nearest_texel clamps an outside tap into the frame), its term selected
+            int32_t vx, vy;
+            nearest_texel(suv, F.s, vx, vy);
+            const float v = D.variance[ch][s_index(F, vx, vy)];
+            const float t = sum_variance + KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
+            sum_variance = (uv_outside(suv) || v > HK_F32_MAX) ? sum_variance : t;
+#endif
         }
         D.internal_variance[ch][idx] = sum_variance;
     }
@@ -2224,7 +2264,8 @@ static dim3 tiles(const Frame& F, uint32_t width, int32_t rows) { return tiles(w
 
 // LDS staging is used when the kernel's scene arrays fit LDS_SCENE_MAX and the kernel gains from
 // it.  Measured on cornell 1080p (1 x MI355X): indirect 0.370 -> 0.317 ms; direct_lit even;
-// direct_emissive 0.167 -> 0.183 ms and the G-buffer even, so those two stay on global loads.
+// direct_emissive 0.167 -> 0.183 ms and the G-buffer even, so those two stay on global loads
+// (round 1, word-by-word staging; round 4: the fused direct launch stages, launch_direct_fused).
 // Option lds_scene: 0 disables staging, 2 stages in every traversal kernel.
 static uint32_t lds_plan_bytes(const FrameArgs& A, int plan, bool preferred)
 {
@@ -2313,7 +2354,9 @@ static void launch_fused_v(const FrameArgs& A, const ChannelArgs& C0, const Chan
 void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, hipStream_t st)
 {
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
-    const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
+    // staged by default since the staging copies chunks with their loads in flight (stage_scene): cornell 1080p
+    // 0.179 -> 0.154 ms, frame 0.363 -> 0.345 ms (profiles/r04/c15, option lds_scene = 2 then)
+    const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, true);
     const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
     const bool ve = validation_frame(A.F.number, A.F.emissive_validate_interval);
     if (lds) launch_fused_v<true>(A, C0, C1, vd, ve, g, lds, st);
@@ -2429,14 +2472,14 @@ void launch_spatial(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit,
     const bool window = A.F.upscale_ratio == 1.0f && A.F.s[0] == A.F.S[0] && A.F.s[1] == A.F.S[1];
     // the view planes hold the indirect channel's records only (ChannelArgs::view)
     if (emissive_lit) {
-        if (window) hipLaunchKernelGGL((k_spatial<true, true, false>), g, dim3(256), 0, st, A, C);
-        else hipLaunchKernelGGL((k_spatial<true, false, false>), g, dim3(256), 0, st, A, C);
+        if (window) hipLaunchKernelGGL((k_spatial<true, false>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial_nowin<true, false>), g, dim3(256), 0, st, A, C);
     } else if (C.view) {
-        if (window) hipLaunchKernelGGL((k_spatial<false, true, true>), g, dim3(256), 0, st, A, C);
-        else hipLaunchKernelGGL((k_spatial<false, false, true>), g, dim3(256), 0, st, A, C);
+        if (window) hipLaunchKernelGGL((k_spatial<false, true>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial_nowin<false, true>), g, dim3(256), 0, st, A, C);
     } else {
-        if (window) hipLaunchKernelGGL((k_spatial<false, true, false>), g, dim3(256), 0, st, A, C);
-        else hipLaunchKernelGGL((k_spatial<false, false, false>), g, dim3(256), 0, st, A, C);
+        if (window) hipLaunchKernelGGL((k_spatial<false, false>), g, dim3(256), 0, st, A, C);
+        else hipLaunchKernelGGL((k_spatial_nowin<false, false>), g, dim3(256), 0, st, A, C);
     }
 }
 void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
