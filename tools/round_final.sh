@@ -24,6 +24,6 @@ else
   timeout -k 10 300 python tools/band_scaling.py cornell-1080p-nee 50 --overhead-ms 0.008 > gpurun_out/$TAG/bands_cornell.log 2>&1
   timeout -k 10 400 python tools/band_scaling.py scene-1080p-full 30 --overhead-ms 0.015 > gpurun_out/$TAG/bands_scene.log 2>&1
   timeout -k 10 600 python tools/band_scaling.py city-4k 30 --overhead-ms 0.037 > gpurun_out/$TAG/bands_city-4k.log 2>&1
-  tail -2 gpurun_out/$TAG/bands_*.log
+  for f in gpurun_out/$TAG/bands_*.log; do tail -n 2 $f; done
   echo round-final-b-done
 fi
