@@ -20,7 +20,7 @@ timeout -k 10 300 python bench.py > $OUT/bench_default.json 2> $OUT/bench_defaul
    --cpu-budget 0 > $R/$OUT/stats_isolated.log 2>&1)
 # the RCCL path itself at world size 1 (communicator, per-frame all-gather, reductions) on the one GPU
 HK_BENCH_DIST=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
-    --master-addr 127.0.0.1 --master-port 29534 bench.py --steps 10 --warmup 3 --cpu-budget 0 > $OUT/rccl_world1.json 2> $OUT/rccl_world1.err
+    --master-addr 127.0.0.1 --master-port 29534 bench.py --cpu-budget 0 > $OUT/rccl_world1.json 2> $OUT/rccl_world1.err
 HK_BENCH_REHEARSAL=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 > $OUT/rehearsal.log 2>&1
 echo final-done
