@@ -299,12 +299,12 @@ def main():
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
     elif dist_on:
-        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 3) of a short
+        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 5) of a short
         # calibration on the current bands — frames 0..5 rendered, 3..5 timed per rank, the times all-gathered
         # — each moving the boundaries to equal measured cost.  Then every rank starts the run from frame 0
         # on its final band (hk_resize zero-fills the reservoirs, as at the start of any run).
         bounds = equal_bounds(world, H)
-        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "3")) if world > 1 else 0):
+        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "5")) if world > 1 else 0):
             b = band_of(rank, world, H, bounds)
             r.resize(W, H, 1.0, b.y0, b.rows)
             for f in range(6):

@@ -11,7 +11,7 @@ The projection adds the collective: one all-gather of the tone-map
 link at ~153 GB/s (MI355X: 7 links x ~153 GB/s per GPU).  bench.py double-buffers it, so the gather of
 frame f runs on RCCL's stream next to frame f+1: frame time = max(compute, gather) when it overlaps,
 compute + gather when it does not; both are printed.
-Row bands are cost-balanced as bench.py balances them (bands.rebalance, --balance R rounds, default 3:
+Row bands are cost-balanced as bench.py balances them (bands.rebalance, --balance R rounds, default 5:
 every rank's band timed, the boundaries moved to equal measured cost, timed again); the equal-row split is
 printed beside it.  --overhead-ms X adds the measured per-frame cost of the collective path itself (the
 band copy, the all-gather's stream waits and the reorder at world size 1: HK_BENCH_DIST=1 minus the
@@ -56,7 +56,7 @@ def arg(name, default):
 out = {"config": cfg_name, "resolution": [W, H], "bands": {}, "allgather_ms": {}, "projected_ms": {},
        "equal_bands": {}, "bounds": {}, "overhead_ms": arg("--overhead-ms", 0.0)}
 only = arg("--only", 0) or None
-rounds = arg("--balance", 3)
+rounds = arg("--balance", 5)
 
 
 def rank_ms(n, rank, stripes, bounds):
