@@ -2156,6 +2156,68 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         lum_rcp[ch] = 1.0f / lum_denom[ch];
         m1[ch] = m2[ch] = cnt[ch] = 0.0f;
     }
+#if HK_DENOISE_PF
+    // The taps in two batches of four: every texel of a batch read first (out-of-frame taps at clamped coordinates,
+    // their values unused), then the batch's taps evaluated exactly as below, branches included.  The empty asm
+    // statement takes the batch's values, so all of its loads are issued before the first is waited for.
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        float4 t0s[4];
+        float sis[4];
+        uint2 irs[4][C];
+        int32_t sxs[4], sys[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * b + j;
+            const int kk = k < 4 ? k : k + 1;
+            const int ox = kk % 3 - 1, oy = kk / 3 - 1;
+            sxs[j] = x + ox * step;
+            sys[j] = y + oy * step;
+            const int32_t sidx = s_index(F, min(max(sxs[j], 0), (int32_t)F.s[0] - 1), min(max(sys[j], 0), (int32_t)F.s[1] - 1));
+            t0s[j] = D.geom[2 * sidx];
+            sis[j] = D.geom[2 * sidx + 1].x;
+#pragma unroll
+            for (int ch = 0; ch < C; ++ch) irs[j][ch] = D.internal[ch][LEVEL][sidx];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            __asm__ volatile("" ::"v"(t0s[j].x), "v"(t0s[j].y), "v"(t0s[j].z), "v"(t0s[j].w), "v"(sis[j]));
+#pragma unroll
+            for (int ch = 0; ch < C; ++ch) __asm__ volatile("" ::"v"(irs[j][ch].x), "v"(irs[j][ch].y));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * b + j;
+            const int kk = k < 4 ? k : k + 1;
+            const int ox = kk % 3 - 1, oy = kk / 3 - 1;
+            const int32_t sx = sxs[j], sy = sys[j];
+            if (sx < 0 || sy < 0 || sx >= (int32_t)F.s[0] || sy >= (int32_t)F.s[1]) continue;
+            const float4 t0 = t0s[j];
+            const float si = sis[j];
+            const float w_normal = hk_pow16(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))));
+            const float w_depth = hk_exp((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
+            const float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
+            const float w_geo = (w_normal * w_depth) * w_instance;
+            const float kw = KERNEL3[oy + 1][ox + 1];
+#pragma unroll
+            for (int ch = 0; ch < C; ++ch) {
+                const uint2 v = irs[j][ch];
+                f3 irr = mk3(unpack_lo16float(v.x), unpack_hi16float(v.x), unpack_lo16float(v.y));
+                if (bad3(irr)) continue;
+                float sl = lum(irr);
+                float w_lum = hk_exp(div_by(-fabsf(l0[ch] - sl), lum_denom[ch], lum_rcp[ch]));
+                float w = hk_clampf(w_geo * w_lum, 0.0f, 1.0f) * kw;
+                sum_irr[ch] = sum_irr[ch] + irr * w;
+                sum_w[ch] += w;
+                if (ch >= 1) {
+                    m1[ch] += sl;
+                    m2[ch] += sl * sl;
+                    cnt[ch] += 1.0f;
+                }
+            }
+        }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int kk = k < 4 ? k : k + 1;  // skip the centre
@@ -2191,6 +2253,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
             }
         }
     }
+#endif
     f4 a = mk4(0, 0, 0, 0);
     if (LEVEL == 3) {
         int32_t gx, gy;
