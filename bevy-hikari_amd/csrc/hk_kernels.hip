@@ -2373,7 +2373,11 @@ static void launch_direct_v(const FrameArgs& A, const ChannelArgs& C, bool val, 
 void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, hipStream_t st)
 {
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
-    const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, false);
+    // staged since round 4 (stage_scene) on frames of >= direct_w4_min_px pixels: cornell 1080p under an orbiting
+    // camera direct_lit 0.110 -> 0.098 ms, emissive 0.124 -> 0.109 ms, frame 0.457 -> 0.413 ms (profiles/r04/c22,
+    // c23); a 256x256 frame (256 workgroups) lost 3 % with it (c23)
+    const bool big = (double)A.F.s[0] * (double)A.F.s_rows >= A.opt.direct_w4_min_px;
+    const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, big);
     if (emissive_lit) {
         const bool val = validation_frame(A.F.number, A.F.emissive_validate_interval);
         if (lds) launch_direct_v<true, false, true>(A, C, val, g, lds, st);
