@@ -247,10 +247,6 @@ HKD Scene stage_scene(const Scene& g, uint32_t* lds)
         (const uint32_t*)g.blas_wide,      (const uint32_t*)g.tlas_wide};
     uint32_t* dst[SCENE_ARRAYS];
     uint4* const lds4 = reinterpret_cast<uint4*>(lds);  // (hk_lds_scene is 16-byte aligned)
-#ifndef HK_STAGE_FLAT
-#define HK_STAGE_FLAT 1
-#endif
-#if HK_STAGE_FLAT
     // The plan's arrays as one list of 16-byte chunks (array k at chunk off4[k], its last chunk rounded up: the
     // bytes read past an array's end lie in the same 16-byte block of its own allocation, and no reader looks at
     // them in LDS), copied four chunks per thread per iteration with the four loads issued before any store
@@ -282,22 +278,6 @@ HKD Scene stage_scene(const Scene& g, uint32_t* lds)
             for (int j = 0; j < 4; ++j) lds4[cs[j]] = v[j];
         }
     }
-#else
-    uint32_t off4 = 0;                                  // in 16-byte units: every array starts on a 16-byte boundary
-#pragma unroll
-    for (int k = 0; k < SCENE_ARRAYS; ++k) {
-        uint4* const d4 = lds4 + off4;
-        dst[k] = reinterpret_cast<uint32_t*>(d4);
-        if (!plan_has(PLAN, k)) continue;
-        const uint32_t words = g.bytes[k] >> 2;
-        // 16-byte copies (the sources are their own allocations), then the few trailing words
-        const uint32_t n4 = words >> 2;
-        const uint4* s4 = reinterpret_cast<const uint4*>(src[k]);
-        for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
-        for (uint32_t i = (n4 << 2) + threadIdx.x; i < words; i += blockDim.x) dst[k][i] = src[k][i];
-        off4 += (words + 3u) >> 2;
-    }
-#endif
     __syncthreads();
     Scene s = g;
     if (plan_has(PLAN, 0)) s.vertices = (const hk_vertex*)dst[0];
@@ -567,13 +547,9 @@ HKD void store_res(const ResBuf& b, int32_t i, const Reservoir& r)
 // results are unchanged; a tested neighbour costs one 16-B gather instead of two and a merged one two or
 // three instead of four.
 constexpr uint32_t VIEW_HIT = 1u << 24, VIEW_COUNT = 1u << 25;
-// HK_VIEW_AOS (experiment builds): the three chunks of a pixel in one 64-byte line (4 x uint4, the fourth
-// unused) instead of three planes, so a merged neighbour's two or three gathers fall in one cache line
-#ifndef HK_VIEW_AOS
-#define HK_VIEW_AOS 0
-#endif
-constexpr uint32_t VIEW_PLANES = HK_VIEW_AOS ? 4u : 3u;  // uint4 chunks allocated per pixel
-HKD uint32_t view_at(uint32_t view_n, uint32_t plane, uint32_t u) { return HK_VIEW_AOS ? 4u * u + plane : plane * view_n + u; }
+// (the three chunks of a pixel in one 64-byte line instead of three planes measured slower: DESIGN §4)
+constexpr uint32_t VIEW_PLANES = 3u;  // uint4 chunks allocated per pixel
+HKD uint32_t view_at(uint32_t view_n, uint32_t plane, uint32_t u) { return plane * view_n + u; }
 HKD void store_res_view(const ResBuf& b, uint4* view, uint32_t view_n, int32_t i, const Reservoir& r)
 {
     uint4 c0, c1, c2, c3;
@@ -798,10 +774,7 @@ HKD void load_triangle(const hk_primitive* prims, uint32_t i, f3& a, f3& b, f3& 
 // the flattened array, bvh flatten).  All STEPS nodes are loaded and tested up front with the
 // same hit distance (no leaf work happens between such visits).  Returns the node the walk visits
 // next; `leaf_pass`/`leaf_entry` report the leaf reached in this iteration, if its box passed.
-#ifndef HK_WALK_STEPS
-#define HK_WALK_STEPS 2
-#endif
-constexpr int WALK_STEPS = HK_WALK_STEPS;  // visits per walk iteration (3 and 4 measured slower)
+constexpr int WALK_STEPS = 2;  // visits per walk iteration (3 and 4 measured slower)
 template <int STEPS>
 HKD uint32_t walk_step(const hk_node* nodes, uint32_t index, uint32_t count, const Ray& tr, float distance,
                        bool& leaf_pass, uint32_t& leaf_entry)
@@ -957,72 +930,6 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
     hit.distance = max_distance;
     hit.instance_index = HK_U32_MAX;
     hit.primitive_index = HK_U32_MAX;
-#if HK_WALK_SELECT
-    uint32_t top = 0u;                  // next TLAS node
-    uint32_t bot = 0u, bot_count = 0u;  // BLAS walk state (in_bottom: inside an instance)
-    uint32_t bot_base = 0u, prim_offset = 0u, cur_instance = 0u;
-    bool in_bottom = false, intersected = false;
-    Ray local = ray;
-    HK_LANE_STATS_DECL;
-    for (;;) {
-        if (!in_bottom && top >= sc.n_instance_nodes) break;
-        HK_LANE_STATS_TICK;
-        const hk_node* nodes = in_bottom ? sc.asset_nodes + bot_base : sc.instance_nodes;
-        const uint32_t count = in_bottom ? bot_count : sc.n_instance_nodes;
-        const uint32_t index = in_bottom ? bot : top;
-        Ray tr;
-        tr.origin = in_bottom ? local.origin : ray.origin;
-        tr.inv_direction = in_bottom ? local.inv_direction : ray.inv_direction;
-        // BLAS leaves carry their triangle's box (k_fill_blas_leaves, light.wgsl:411-413), TLAS
-        // leaves their instance's min/max (k_fill_tlas_leaves, light.wgsl:456-457); the leaf this
-        // iteration reaches (if any) and the node after it
-        bool leaf_pass;
-        uint32_t leaf_entry;
-        const uint32_t next = walk_step<WALK_STEPS>(nodes, index, count, tr, hit.distance, leaf_pass, leaf_entry);
-        if (in_bottom) {
-            bool stop = false;
-            if (leaf_pass) {
-                const uint32_t primitive_index = prim_offset + leaf_entry - HK_BVH_LEAF_FLAG;
-                f3 a, b, c;
-                load_triangle(sc.primitives, primitive_index, a, b, c);
-                f2 uv;
-                const float d = intersects_triangle(local, a, b, c, uv);
-                if (d < hit.distance) {
-                    hit.distance = d;
-                    hit.uv = uv;
-                    hit.primitive_index = primitive_index;
-                    intersected = true;
-                    stop = d < early_distance;  // traverse_bottom's early return
-                }
-            }
-            bot = next;
-            if (stop || bot >= bot_count) {  // back in traverse_top after traverse_bottom
-                in_bottom = false;
-                if (intersected) {
-                    hit.instance_index = cur_instance;
-                    if (hit.distance < early_distance) return hit;
-                }
-            }
-        } else {
-            top = next;
-            const uint32_t instance_index = leaf_entry - HK_BVH_LEAF_FLAG;
-            if (leaf_pass && instance_index != exclude) {
-                const hk_instance& in = sc.instances[instance_index];
-                local.origin = world_to_local_point(in, ray.origin);
-                local.direction = world_to_local_dir(in, ray.direction);
-                local.inv_direction = inv(local.direction);
-                bot = 0u;
-                bot_count = in.mesh.node[1];
-                bot_base = in.mesh.node[0];
-                prim_offset = in.mesh.primitive;
-                cur_instance = instance_index;
-                intersected = false;
-                in_bottom = bot_count > 0u;  // traverse_bottom over an empty range does nothing
-            }
-        }
-    }
-    return hit;
-#else
     // The walk in progress — the TLAS, or the BLAS of the instance being visited — as one set of registers (its
     // nodes, length, position and ray), switched when the walk enters or leaves an instance, so that an iteration
     // selects nothing between the two levels' states.
@@ -1090,7 +997,6 @@ HKD Hit traverse_top(const Scene& sc, const Ray& ray, float max_distance, float 
         }
     }
     return hit;
-#endif
 }
 
 // ------------------------------------------------------------------ G-buffer visibility

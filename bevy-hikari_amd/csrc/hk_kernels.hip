@@ -21,24 +21,6 @@
 
 namespace hk {
 
-#ifdef HK_LANE_STATS
-__device__ unsigned long long hk_lane_stats_dev[2];
-#endif
-// traverse_top lane statistics since the last call (instrumented builds; false otherwise)
-bool lane_stats_take(unsigned long long out[2], hipStream_t st)
-{
-#ifdef HK_LANE_STATS
-    unsigned long long zero[2] = {0, 0};
-    if (hipStreamSynchronize(st) != hipSuccess) return false;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hk_lane_stats_dev), sizeof(zero)) != hipSuccess) return false;
-    return hipMemcpyToSymbol(HIP_SYMBOL(hk_lane_stats_dev), zero, sizeof(zero)) == hipSuccess;
-#else
-    (void)st;
-    out[0] = out[1] = 0;
-    return false;
-#endif
-}
-
 // workgroup -> 16x16 tile -> pixel (global coordinates).  Tile orders:
 // RASTER: blockIdx in raster order; workgroups are dealt round-robin over the 8 XCDs, so every
 //   XCD works on the same band of the frame at once and per-region cost differences (sky vs.
@@ -53,10 +35,7 @@ bool lane_stats_take(unsigned long long out[2], hipStream_t st)
 //   order their +/- 20-row window of reservoirs (~7 MB at 1080p) does not fit it.  The a-trous
 //   levels use it too (city 4K: 0.529 -> 0.436 ms per level).
 enum TileOrder : int { RASTER = 0, XCD_RASTER = 1, XCD_STRIPS = 2 };
-#ifndef HK_STRIP_TILES
-#define HK_STRIP_TILES 16
-#endif
-constexpr uint32_t STRIP_TILES = HK_STRIP_TILES;
+constexpr uint32_t STRIP_TILES = 16;  // 8 / 32 / 64 measured slower
 template <int ORDER>
 HKD void tile_coords_at(uint32_t bx, uint32_t by, uint32_t gx, uint32_t gy, uint32_t& tx, uint32_t& ty)
 {
@@ -107,41 +86,6 @@ HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, 
     return tile_pixel_at<ORDER>(F, width, row0, rows, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, x, y);
 }
 
-// Occupancy hints for the traversal kernels (waves per SIMD); tunable at build time.
-#ifndef HK_TRACE_WAVES
-#define HK_TRACE_WAVES 0
-#endif
-#if HK_TRACE_WAVES > 0
-#define HK_TRACE_OCC __attribute__((amdgpu_waves_per_eu(HK_TRACE_WAVES, 8)))
-#else
-#define HK_TRACE_OCC
-#endif
-// per-kernel overrides (waves per SIMD the register allocator must allow)
-#ifndef HK_DIRECT_WAVES
-#define HK_DIRECT_WAVES 0
-#endif
-#ifndef HK_INDIRECT_WAVES
-#define HK_INDIRECT_WAVES 0
-#endif
-#if HK_DIRECT_WAVES > 0
-#define HK_DIRECT_OCC __attribute__((amdgpu_waves_per_eu(HK_DIRECT_WAVES, 8)))
-#else
-#define HK_DIRECT_OCC HK_TRACE_OCC
-#endif
-#if HK_INDIRECT_WAVES > 0
-#define HK_INDIRECT_OCC __attribute__((amdgpu_waves_per_eu(HK_INDIRECT_WAVES, 8)))
-#else
-#define HK_INDIRECT_OCC HK_TRACE_OCC
-#endif
-#ifndef HK_SPATIAL_WAVES
-#define HK_SPATIAL_WAVES 0
-#endif
-#if HK_SPATIAL_WAVES > 0
-#define HK_SPATIAL_OCC __attribute__((amdgpu_waves_per_eu(HK_SPATIAL_WAVES, 8)))
-#else
-#define HK_SPATIAL_OCC HK_TRACE_OCC
-#endif
-
 // origin (global coordinates, contiguous bands) of this workgroup's tile
 template <int ORDER = RASTER>
 HKD void tile_origin(const Frame& F, int32_t row0, int32_t& x0, int32_t& y0)
@@ -151,15 +95,9 @@ HKD void tile_origin(const Frame& F, int32_t row0, int32_t& x0, int32_t& y0)
     x0 = (int32_t)(tx * 16u);
     y0 = row0 + (F.win_rows > 0 ? F.win_row0 : 0) + (int32_t)(ty * 16u);
 }
-#ifndef HK_SPATIAL_ORDER
-#define HK_SPATIAL_ORDER XCD_STRIPS
-#endif
-#ifndef HK_TRACE_ORDER  // G-buffer and light-pass kernels
-#define HK_TRACE_ORDER RASTER
-#endif
-#ifndef HK_DENOISE_ORDER  // the a-trous levels (taps up to 8 px away): city 4K 0.529 -> 0.436 ms per level
-#define HK_DENOISE_ORDER XCD_STRIPS
-#endif
+constexpr int SPATIAL_ORDER = XCD_STRIPS;  // spatial reuse: neighbour reservoirs +/- 20 px in one XCD's L2
+constexpr int TRACE_ORDER = RASTER;        // G-buffer and light-pass kernels
+constexpr int DENOISE_ORDER = XCD_STRIPS;  // the a-trous levels (taps up to 8 px away): city 4K 0.529 -> 0.436 ms per level
 
 // ------------------------------------------------------------------ G-buffer
 HKD f3 primary_direction(const ViewArgs& V, float px, float py, const uint32_t* size)
@@ -213,7 +151,7 @@ HKD f4 albedo_of(const Frame& F, const Scene& sc, f4 pd, uint32_t packed_normal,
 
 // albedo != null: the frame's full_screen_albedo is written here too (hk_render_frame skips it)
 template <bool LDS, bool SHALLOW, int LVL = GB_STACK_LDS>
-__global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewArgs V, uint2* albedo)
+__global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V, uint2* albedo)
 {
     // The traversal stack's LDS levels, in the launch's dynamic LDS (entry-major, [level][256]): every
     // level of the scene's stack bound for SHALLOW (launch_gbuffer sizes it: a shallow scene's
@@ -225,7 +163,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
     if constexpr (LDS) sc = stage_scene<PLAN_GBUFFER>(A.sc, hk_lds_scene);
     else sc = A.sc;
     int32_t x, y;
-    bool active = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
+    bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y);
     uint32_t n_primary = 0;
     if (active) {
         n_primary = 1;
@@ -296,7 +234,7 @@ __global__ __launch_bounds__(256) HK_TRACE_OCC void k_gbuffer(FrameArgs A, ViewA
 __global__ __launch_bounds__(256) void k_albedo(FrameArgs A, uint2* albedo)
 {
     int32_t x, y;
-    if (!tile_pixel<HK_TRACE_ORDER>(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
+    if (!tile_pixel<TRACE_ORDER>(A.F, A.F.S[0], A.F.S_row0, A.F.S_rows, x, y)) return;
     const int32_t idx = band_index(A.F, x, y, A.F.S[0], A.F.S_row0, A.F.S_rows);
     const f4 pd = load_position(A.F, A.G, x, y);
     if (pd.w < HK_F32_EPSILON) {
@@ -700,14 +638,14 @@ HKD void direct_pass(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
 }
 
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS, bool VALIDATE>
-__global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
 {
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_pass<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -718,9 +656,6 @@ __global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct(FrameArgs A, Chann
 // same body with 4 waves per SIMD for the separate-launch path (bands / stripes) when the grid
 // has enough waves to use them (>= 400 K pixels): cornell 2-way stripe 0.348 -> 0.328 ms/frame,
 // 4-way 0.192 -> 0.187; an 8-way stripe (259 K pixels, about one wave per slot) 0.1455 -> 0.1474
-#ifndef HK_DIRECT_LIT_W4
-#define HK_DIRECT_LIT_W4 1
-#endif
 // (the threshold is LaunchOpts::direct_w4_min_px)
 template <bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_lit_w4(FrameArgs A, ChannelArgs C)
@@ -730,7 +665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_pass<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -743,14 +678,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // 1: the G-buffer of k_gbuffer), so per-thread program order is the reference's pass order for
 // every stored word; the runtime uses it only then.  One launch and one tail instead of two.
 template <bool LDS, bool VD, bool VE>
-__global__ __launch_bounds__(256) HK_DIRECT_OCC void k_direct_fused(FrameArgs A, ChannelArgs C0, ChannelArgs C1)
+__global__ __launch_bounds__(256) void k_direct_fused(FrameArgs A, ChannelArgs C0, ChannelArgs C1)
 {
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
+    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
         const DirectPixel P = load_direct_pixel(A, x, y);
         const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
         if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
@@ -783,7 +718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     else sc = A.sc;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
+    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
         const DirectPixel P = load_direct_pixel(A, x, y);
         const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
         if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
@@ -971,7 +906,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     float* lds = VD ? park_area() : cw_area();
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    const bool on = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    const bool on = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
     DirectPixel P;
     uint32_t bg = BG_SKIP_ALL;
     if (on) {
@@ -1365,10 +1300,10 @@ HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C
 
 // CS: the one-bounce path's shadow walks compacted per workgroup (compact_top_walks; option compact_shadow)
 template <bool MULTI, bool LDS, bool CS = false>
-__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
-    const bool active = tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
     Scene sc = A.sc;
     if constexpr (LDS) {
         sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
@@ -1432,7 +1367,7 @@ HKD void persist_tiles(const FrameArgs& A, uint32_t kind, Body body)
     }
 }
 template <bool MULTI, bool LDS>
-__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_indirect_persist(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) void k_indirect_persist(FrameArgs A, ChannelArgs C)
 {
     Scene sc = A.sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
@@ -1467,7 +1402,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const uint32_t bx = zsplit ? blockIdx.x : blockIdx.x >> 1, gx = zsplit ? gridDim.x : gridDim.x >> 1;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    const bool active = tile_pixel_at<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, bx, blockIdx.y, gx, gridDim.y, x, y);
+    const bool active = tile_pixel_at<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, bx, blockIdx.y, gx, gridDim.y, x, y);
     if (zsplit ? blockIdx.z == 0u : (blockIdx.x & 1u) != 0u) {
         Scene sc = A.sc;
         if constexpr (LDS_I) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
@@ -1551,7 +1486,7 @@ __global__ __launch_bounds__(256) void k_wf_gen(FrameArgs A, ChannelArgs C, WfAr
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     bool live = false;
-    if (tile_pixel<HK_TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
+    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         live = indirect_body<false, IND_GEN>(A, A.sc, C, x, y, n_top, n_emitter);
     const uint64_t m = __ballot(live);
     const uint32_t wave = threadIdx.x >> 6;
@@ -1573,7 +1508,7 @@ __global__ __launch_bounds__(256) void k_wf_gen(FrameArgs A, ChannelArgs C, WfAr
 }
 
 template <bool LDS>
-__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_wf_trace(FrameArgs A, ChannelArgs C, WfArgs W)
+__global__ __launch_bounds__(256) void k_wf_trace(FrameArgs A, ChannelArgs C, WfArgs W)
 {
     uint32_t seg, i;
     const bool valid = wf_entry(W, seg, i);
@@ -1634,7 +1569,7 @@ __global__ __launch_bounds__(256) void k_wf_scatter(WfArgs W)
 }
 
 template <bool LDS>
-__global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_wf_shade(FrameArgs A, ChannelArgs C, WfArgs W)
+__global__ __launch_bounds__(256) void k_wf_shade(FrameArgs A, ChannelArgs C, WfArgs W)
 {
     const uint32_t n = W.ctl[WF_SEGS];
     if (blockIdx.x * 256u >= n) return;
@@ -1663,15 +1598,9 @@ __global__ __launch_bounds__(256) HK_INDIRECT_OCC void k_wf_shade(FrameArgs A, C
 // loads per pixel.  Values are load_depth() of the same coordinates (frame-OOB -> 0, band
 // clamp), so results are unchanged; a coordinate outside the window reads global memory.
 constexpr int32_t SP_HALO = 22, SP_WIN = 16 + 2 * SP_HALO;
-// HK_SP_P0WIN (experiment builds): the indirect spatial pass also stages view plane 0 of its window in LDS
-// (57.6 KiB per workgroup besides the depth window: 2 workgroups per CU instead of 5)
-#ifndef HK_SP_P0WIN
-#define HK_SP_P0WIN 0
-#endif
 struct DepthWin {
     const float* lds;  // null: no window (upscale ratio != 1)
     int32_t x0, y0;
-    const uint4* p0;   // HK_SP_P0WIN: view plane 0 of the window, or null
 };
 HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t x, int32_t y)
 {
@@ -1764,13 +1693,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     const float srand = sum4(s.random);
     const f3 s_visible = xyz(s.visible_position);
     const f3 s_normal = s.visible_normal;
-#if defined(HK_LANE_STATS) && defined(HK_SP_STATS)
-    LaneStats lane_stats_;
-#endif
     for (uint32_t i = 1u; i <= COUNT; i += 1u) {
-#if defined(HK_LANE_STATS) && HK_SP_STATS == 0  // lane statistics per neighbour iteration (experiments)
-        lane_stats_.tick();
-#endif
         float px = HK_TAU * hk_fract(((float)i * HK_GOLDEN_RATIO + srand) + rf);
         const float py = F.sp_py[EMISSIVE_LIT][i - 1u];  // sqrt(i / COUNT) * RANGE
         float sn, cs;
@@ -1800,9 +1723,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         const float tap_interval = F.sp_tap_interval[EMISSIVE_LIT][i - 1u];  // max(1, py / 5)
         uint32_t tap_count = F.sp_tap_count[EMISSIVE_LIT][i - 1u];          // u32(py / tap_interval)
         bool occluded = false;
-#if defined(HK_LANE_STATS) && HK_SP_STATS == 1  // lane statistics at the occlusion march (experiments)
-        lane_stats_.tick();
-#endif
         float inv_len = 1.0f / sqrtf(dot(offset, offset));
         f2 dir = mk2(offset.x * inv_len, offset.y * inv_len);
         const float sx = (float)F.s[0], sy = (float)F.s[1];
@@ -1841,8 +1761,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         bool count_ok;
         f3 q_sample;
         if constexpr (VIEW) {
-            const uint4 a = (HK_SP_P0WIN && WINDOW) ? W.p0[(scy - W.y0) * SP_WIN + (scx - W.x0)]
-                                                    : C.view[view_at(C.view_n, 0u, (uint32_t)nidx)];
+            const uint4 a = C.view[view_at(C.view_n, 0u, (uint32_t)nidx)];
             normal_word = a.w;
             count_ok = (a.w & VIEW_COUNT) != 0u;
             q_sample = mk3(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
@@ -1962,11 +1881,10 @@ template <bool EMISSIVE_LIT, bool WINDOW, bool VIEW>
 HKD void spatial_kernel(const FrameArgs& A, const ChannelArgs& C)
 {
     __shared__ float win[WINDOW ? SP_WIN * SP_WIN : 1];
-    __shared__ uint4 p0win[(HK_SP_P0WIN && WINDOW && VIEW) ? SP_WIN * SP_WIN : 1];
-    DepthWin W{nullptr, 0, 0, nullptr};
+    DepthWin W{nullptr, 0, 0};
     if (WINDOW) {
         int32_t x0, y0;
-        tile_origin<HK_SPATIAL_ORDER>(A.F, A.F.s_row0, x0, y0);
+        tile_origin<SPATIAL_ORDER>(A.F, A.F.s_row0, x0, y0);
         W.x0 = x0 - SP_HALO;
         W.y0 = y0 - SP_HALO;
         // load_depth of the 3600 window texels, 15 per thread: all 15 loads issued before any LDS store (at
@@ -1999,36 +1917,24 @@ HKD void spatial_kernel(const FrameArgs& A, const ChannelArgs& C)
             const int32_t k = (int32_t)threadIdx.x + j * 256;
             if (j < PER - 1 || k < N) win[k] = v[j];
         }
-        if constexpr (HK_SP_P0WIN && VIEW) {
-            for (int32_t k = (int32_t)threadIdx.x; k < SP_WIN * SP_WIN; k += 256) {
-                const int32_t wx = W.x0 + k % SP_WIN, wy = W.y0 + k / SP_WIN;
-                // the neighbour test's frame bounds; s_index clamps to the band's rows as the gather does
-                const bool in = wx >= 0 && wy >= 0 && wx < (int32_t)A.F.s[0] && wy < (int32_t)A.F.s[1];
-                p0win[k] = in ? C.view[view_at(C.view_n, 0u, (uint32_t)s_index(A.F, wx, wy))] : make_uint4(0, 0, 0, 0);
-            }
-            W.p0 = p0win;
-        }
         __syncthreads();
         W.lds = win;
     }
     int32_t x, y;
-    if (tile_pixel<HK_SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT, WINDOW, VIEW>(A, C, x, y, W);
+    if (tile_pixel<SPATIAL_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) spatial_body<EMISSIVE_LIT, WINDOW, VIEW>(A, C, x, y, W);
 }
 // The window variant (upscale ratio 1) at 6 waves per SIMD: its neighbour loop fits 78 VGPRs without spilling once
 // the window staging no longer holds 15 loads' worth of state per texel loop (city 4K 1.587 -> 1.481 ms, scene
 // 0.489 -> 0.464 ms, profiles/r04/c15; the 14.4 KiB window allows 11 workgroups per CU).  The variant without the
 // window (upscale ratio 2, host G-buffers) would spill there and keeps the compiler's choice.
-#ifndef HK_SPATIAL_WIN_WAVES
-#define HK_SPATIAL_WIN_WAVES 6
-#endif
 template <bool EMISSIVE_LIT, bool VIEW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HK_SPATIAL_WIN_WAVES, 8))) void k_spatial(FrameArgs A,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_spatial(FrameArgs A,
                                                                                                              ChannelArgs C)
 {
     spatial_kernel<EMISSIVE_LIT, true, VIEW>(A, C);
 }
 template <bool EMISSIVE_LIT, bool VIEW>
-__global__ __launch_bounds__(256) HK_SPATIAL_OCC void k_spatial_nowin(FrameArgs A, ChannelArgs C)
+__global__ __launch_bounds__(256) void k_spatial_nowin(FrameArgs A, ChannelArgs C)
 {
     spatial_kernel<EMISSIVE_LIT, false, VIEW>(A, C);
 }
@@ -2070,12 +1976,6 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
     f2 duv = jittered_uv(F, uv, 0.5f);
     int32_t ax, ay, rx, ry;
     nearest_texel(duv, F.S, ax, ay);
-#if HK_DEMOD_BRANCHY
-    // geometry the denoise levels read for this pixel (denoise.wgsl:220-223, 197-200)
-    store_geom(D, idx, normalize(load_normal(F, A.G, ax, ay)), load_depth(F, A.G, ax, ay),
-               load_instance_material(F, A.G, ax, ay).x, load_depth_gradient(F, A.G, ax, ay));
-    f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
-#else
     // (ax, ay) is a nearest_texel: inside the frame, so the load_* bounds tests always pass; the texels are read
     // directly, without their branch regions, so all of them are in flight together (same texels, same values)
     {
@@ -2086,7 +1986,6 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
         store_geom(D, idx, normalize(normal), A.G.position[g].w, A.G.instance_material[g].x, mk2(grad.x, grad.y));
     }
     f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
-#endif
     nearest_texel(uv, F.s, rx, ry);
     const int32_t ridx = s_index(F, rx, ry);
 #pragma unroll
@@ -2100,21 +1999,12 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
         for (int k = 0; k < 9; ++k) {
             const int ox = k / 3 - 1, oy = k % 3 - 1;  // (-1,-1),(-1,0),(-1,1),(0,-1),...
             f2 suv = mk2(uv.x + (float)ox / (float)F.s[0], uv.y + (float)oy / (float)F.s[1]);
-#if HK_DEMOD_BRANCHY
-            if (uv_outside(suv)) continue;
-            int32_t vx, vy;
-            nearest_texel(suv, F.s, vx, vy);
-            float v = D.variance[ch][s_index(F, vx, vy)];
-            if (v > HK_F32_MAX) continue;
-            sum_variance += KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
-#else
             // every tap read (nearest_texel clamps an outside tap into the frame), its term selected
             int32_t vx, vy;
             nearest_texel(suv, F.s, vx, vy);
             const float v = D.variance[ch][s_index(F, vx, vy)];
             const float t = sum_variance + KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
             sum_variance = (uv_outside(suv) || v > HK_F32_MAX) ? sum_variance : t;
-#endif
         }
         D.internal_variance[ch][idx] = sum_variance;
     }
@@ -2125,7 +2015,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     const Frame& F = A.F;
     int32_t x, y;
-    if (!tile_pixel<HK_DENOISE_ORDER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    if (!tile_pixel<DENOISE_ORDER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
     constexpr int32_t step = 8 >> LEVEL;
     const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
@@ -2384,7 +2274,7 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
         else launch_direct_v<true, false, false>(A, C, val, g, 0, st);
     } else {
         const bool val = validation_frame(A.F.number, A.F.direct_validate_interval);
-        if (HK_DIRECT_LIT_W4 && (double)A.F.s[0] * (double)A.F.s_rows >= A.opt.direct_w4_min_px) {
+        if ((double)A.F.s[0] * (double)A.F.s_rows >= A.opt.direct_w4_min_px) {
             if (lds) {
                 if (val) hipLaunchKernelGGL((k_direct_lit_w4<true, true>), g, dim3(256), lds, st, A, C);
                 else hipLaunchKernelGGL((k_direct_lit_w4<true, false>), g, dim3(256), lds, st, A, C);

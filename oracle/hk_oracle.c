@@ -162,6 +162,10 @@ struct hko_ctx {
     hk_counters counters;
     int32_t band_y0, band_y1; /* rows computed by every pass (whole frame by default) */
     int32_t stripe_n, stripe_k; /* hko_set_stripes: only rows of 8-row stripes k, k + n, ... (n >= 2) */
+    /* the closest-hit light walks (the indirect bounce, light.wgsl:1319,1401; the emitter BLAS walk of
+     * select_light_candidate, light.wgsl:687): hko_set_light_walk */
+    int light_walk;
+    unsigned long long walk_checked[2], walk_differ[2]; /* [bounce, emitter], light_walk == HKO_WALK_CHECK */
 };
 
 typedef struct {
@@ -567,6 +571,70 @@ static Hit traverse_top(const hko_ctx* c, Counts* cnt, const Ray* ray, float max
     return hit;
 }
 
+/* The closest-hit light walks.  light.wgsl walks them with the stackless skip-pointer order of
+ * traverse_top / traverse_bottom (light.wgsl:400-486): the bounce ray (`traverse_top(ray, F32_MAX, 0.0,
+ * DONT_EXCLUDE)`, light.wgsl:1319,1401) and the emitter BLAS walk (`traverse_bottom(..., 0.0)`,
+ * light.wgsl:687).  Neither has an early exit, so the hit they return is the closest one whatever the
+ * visit order, except for exact-distance ties and box tests that round across the hit distance.  The
+ * HIP kernels walk the bounce ray with the G-buffer's ordered rule (closest_hit_ordered: nearer child
+ * first, the farther pushed and dropped on pop once it cannot win).  hko_set_light_walk selects:
+ *   HKO_WALK_REFERENCE  light.wgsl's order for both;
+ *   HKO_WALK_ORDERED    the bounce walk with the ordered rule (what the HIP kernels run);
+ *   HKO_WALK_CHECK      light.wgsl's order, and every bounce ray and emitter walk walked with the ordered rule
+ *                       too; the rays whose two results differ in any bit (instance, primitive, distance, uv)
+ *                       are counted (hko_light_walk_stats).  Zero bounce differences on a workload pin the
+ *                       kernels' ordered bounce walk to light.wgsl's results there (tests/test_light_walks.py);
+ *                       the emitter count is analysis only: the kernels keep light.wgsl's order for the emitter
+ *                       walk, which aims at sampled emitter points, shared triangle edges included, where the
+ *                       ordered rule breaks ties differently. */
+static Hit closest_hit_ordered(const hko_ctx* c, const Ray* ray);
+static int emitter_walk_ordered(const hko_ctx* c, Hit* hit, const Ray* ray, const hk_mesh_index* mesh);
+static int hit_differs(const Hit* a, const Hit* b)
+{
+    return a->instance_index != b->instance_index || a->primitive_index != b->primitive_index ||
+           hk_f2u(a->intersection.distance) != hk_f2u(b->intersection.distance) ||
+           hk_f2u(a->intersection.uv.x) != hk_f2u(b->intersection.uv.x) ||
+           hk_f2u(a->intersection.uv.y) != hk_f2u(b->intersection.uv.y);
+}
+static void walk_tally(const hko_ctx* c, int k, int differ)
+{
+    hko_ctx* m = (hko_ctx*)c; /* counters only */
+    __atomic_fetch_add(&m->walk_checked[k], 1ull, __ATOMIC_RELAXED);
+    if (differ) __atomic_fetch_add(&m->walk_differ[k], 1ull, __ATOMIC_RELAXED);
+}
+/* the bounce ray: traverse_top(ray, F32_MAX, 0.0, DONT_EXCLUDE) */
+static Hit bounce_walk(const hko_ctx* c, Counts* cnt, const Ray* ray)
+{
+    if (c->light_walk == HKO_WALK_ORDERED) {
+        cnt->top++;
+#ifdef HKO_STATS
+        hko_class = 0;
+        HKO_STAT(0);
+#endif
+        return closest_hit_ordered(c, ray);
+    }
+    Hit h = traverse_top(c, cnt, ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+    if (c->light_walk == HKO_WALK_CHECK) {
+        Hit o = closest_hit_ordered(c, ray);
+        walk_tally(c, 0, hit_differs(&h, &o));
+    }
+    return h;
+}
+/* the emitter BLAS walk: traverse_bottom(hit, r, mesh, 0.0) from an empty hit */
+static int emitter_walk(const hko_ctx* c, Hit* hit, const Ray* r, const hk_mesh_index* mesh)
+{
+    Hit start = *hit;
+    int traced = traverse_bottom(c, hit, r, *mesh, 0.0f);
+    if (c->light_walk == HKO_WALK_CHECK) {
+        Hit o = start;
+        int t2 = emitter_walk_ordered(c, &o, r, mesh);
+        /* the instance field is the caller's (light.wgsl:689) */
+        o.instance_index = hit->instance_index;
+        walk_tally(c, 1, t2 != traced || hit_differs(hit, &o));
+    }
+    return traced;
+}
+
 static HitInfo empty_hit_info(v3 position, v3 direction)
 {
     HitInfo info;
@@ -756,7 +824,7 @@ static LightCandidate select_light_candidate(const Pass* P, Counts* cnt, v4 rand
             hko_class = 3;
             HKO_STAT(0);
 #endif
-            traced = traverse_bottom(c, &hit, &r, emissive_instance->mesh, 0.0f);
+            traced = emitter_walk(c, &hit, &r, &emissive_instance->mesh);
         }
         if (traced) {
             hit.instance_index = emissive->instance;
@@ -1242,7 +1310,7 @@ static void indirect_lit_ambient(const Pass* P, Counts* cnt, int32_t x, int32_t 
             normal_basis(bounce_sample.visible_normal, &bt, &bb);
             ray.direction = basis_mul(bt, bb, bounce_sample.visible_normal, xyz(rand_sample));
             ray.inv_direction = inv3(ray.direction);
-            hit = traverse_top(c, cnt, &ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+            hit = bounce_walk(c, cnt, &ray);
             info = hit_info(c, &ray, &hit);
             if (n == 0u) {
                 s.sample_position = info.position;
@@ -1302,7 +1370,7 @@ static void indirect_lit_ambient(const Pass* P, Counts* cnt, int32_t x, int32_t 
         normal_basis(s.visible_normal, &bt, &bb);
         ray.direction = basis_mul(bt, bb, s.visible_normal, xyz(rand_sample));
         ray.inv_direction = inv3(ray.direction);
-        hit = traverse_top(c, cnt, &ray, HK_F32_MAX, 0.0f, DONT_EXCLUDE);
+        hit = bounce_walk(c, cnt, &ray);
         info = hit_info(c, &ray, &hit);
         s.sample_position = info.position;
         s.sample_normal = info.normal;
@@ -1569,6 +1637,7 @@ static void closest_bottom_ordered(const hko_ctx* c, GbStack* s, Hit* hit, const
     if (mesh->node[1] == 0) return;
     uint32_t p = base;
     for (;;) {
+        HKO_STAT(3);
         const hk_node* node = &c->asset_nodes[p];
         int go = 0;
         if (node->entry_index >= HK_BVH_LEAF_FLAG) {
@@ -1577,6 +1646,7 @@ static void closest_bottom_ordered(const hko_ctx* c, GbStack* s, Hit* hit, const
             v3 a = ld3(v[0].position), e = ld3(v[1].position), d = ld3(v[2].position);
             Aabb box = {min3(a, min3(e, d)), max3(a, max3(e, d))};
             if (intersects_aabb(ray, box) < hit->intersection.distance) {
+                HKO_STAT(4);
                 Intersection is = intersects_triangle(ray, v);
                 if (is.distance < hit->intersection.distance) {
                     hit->intersection = is;
@@ -1603,6 +1673,7 @@ static Hit closest_hit_ordered(const hko_ctx* c, const Ray* ray)
     s.sp = 0;
     uint32_t p = 0;
     for (;;) {
+        HKO_STAT(1);
         const hk_node* node = &c->instance_nodes[p];
         int go = 0;
         if (node->entry_index >= HK_BVH_LEAF_FLAG) {
@@ -1614,6 +1685,7 @@ static Hit closest_hit_ordered(const hko_ctx* c, const Ray* ray)
                 r.origin = instance_position_world_to_local(instance, ray->origin);
                 r.direction = instance_direction_world_to_local(instance, ray->direction);
                 r.inv_direction = inv3(r.direction);
+                HKO_STAT(2);
                 closest_bottom_ordered(c, &s, &hit, &r, &instance->mesh, instance_index);
             }
         } else {
@@ -1622,6 +1694,19 @@ static Hit closest_hit_ordered(const hko_ctx* c, const Ray* ray)
         if (go) continue;
         if (!gb_pop(&s, 0, hit.intersection.distance, &p)) return hit;
     }
+}
+
+/* the emitter BLAS walk with the ordered rule: closest_bottom_ordered from an empty stack; traced iff a
+ * triangle replaced the empty hit (traverse_bottom's `intersected`) */
+static int emitter_walk_ordered(const hko_ctx* c, Hit* hit, const Ray* ray, const hk_mesh_index* mesh)
+{
+    GbStack s;
+    s.sp = 0;
+    const uint32_t before = hit->primitive_index;
+    const float d0 = hit->intersection.distance;
+    const uint32_t inst = hit->instance_index;
+    closest_bottom_ordered(c, &s, hit, ray, mesh, inst);
+    return hit->intersection.distance < d0 || hit->primitive_index != before;
 }
 
 static v3 primary_direction(const hk_view* view, float px, float py, const uint32_t* size)
@@ -2298,6 +2383,19 @@ void hko_set_stripes(hko_ctx* c, int32_t rank, int32_t world)
 }
 
 void hko_counters(hko_ctx* c, hk_counters* out) { *out = c->counters; }
+void hko_set_light_walk(hko_ctx* c, int mode)
+{
+    c->light_walk = mode;
+    memset(c->walk_checked, 0, sizeof(c->walk_checked));
+    memset(c->walk_differ, 0, sizeof(c->walk_differ));
+}
+void hko_light_walk_stats(const hko_ctx* c, unsigned long long* out)
+{
+    out[0] = c->walk_checked[0];
+    out[1] = c->walk_differ[0];
+    out[2] = c->walk_checked[1];
+    out[3] = c->walk_differ[1];
+}
 void hko_reset_counters(hko_ctx* c) { memset(&c->counters, 0, sizeof(c->counters)); }
 
 void hko_trace(hko_ctx* c, const float* rays, const float* max_distance, const float* early_distance,
@@ -2325,6 +2423,25 @@ void hko_trace(hko_ctx* c, const float* rays, const float* max_distance, const f
 #ifdef HKO_STATS
         if (hko_steps_out) hko_steps_out[i] = hko_ray_steps;
 #endif
+    }
+}
+
+/* hko_trace's closest-hit rays (no early exit, nothing excluded) with the ordered rule: 5 words per ray as hko_trace */
+void hko_trace_ordered(hko_ctx* c, const float* rays, uint32_t n, void* hits)
+{
+#pragma omp parallel for schedule(static) HKO_THREADS(c)
+    for (long long i = 0; i < (long long)n; ++i) {
+        Ray ray;
+        ray.origin = ld3(rays + 6 * i);
+        ray.direction = ld3(rays + 6 * i + 3);
+        ray.inv_direction = inv3(ray.direction);
+        Hit h = closest_hit_ordered(c, &ray);
+        uint32_t* o = (uint32_t*)hits + 5 * i;
+        o[0] = hk_f2u(h.intersection.uv.x);
+        o[1] = hk_f2u(h.intersection.uv.y);
+        o[2] = hk_f2u(h.intersection.distance);
+        o[3] = h.instance_index;
+        o[4] = h.primitive_index;
     }
 }
 

@@ -55,11 +55,19 @@ void* hko_output(hko_ctx* ctx, int output_id, uint32_t* width, uint32_t* height,
 hk_packed_reservoir* hko_reservoirs(hko_ctx* ctx, int id, uint32_t* count);
 void hko_counters(hko_ctx* ctx, hk_counters* out);
 void hko_reset_counters(hko_ctx* ctx);
+/* the closest-hit light walks: light.wgsl's order, the bounce walk with the ordered rule (as the HIP kernels), or
+ * light.wgsl's order with every bounce and emitter walk also walked with the ordered rule and the differing rays
+ * counted; stats = {bounce rays checked, differing, emitter walks checked, differing} */
+enum { HKO_WALK_REFERENCE = 0, HKO_WALK_ORDERED = 1, HKO_WALK_CHECK = 2 };
+void hko_set_light_walk(hko_ctx* ctx, int mode);
+void hko_light_walk_stats(const hko_ctx* ctx, unsigned long long* stats);
 
 /* light.wgsl:442-486 for n rays {origin, direction}; hits {u, v, t, instance, primitive} */
 void hko_primary_hits(hko_ctx* ctx, const hk_frame_inputs* in, uint32_t* out);
 void hko_trace(hko_ctx* ctx, const float* rays, const float* max_distance, const float* early_distance,
                const uint32_t* exclude_instance, uint32_t n, void* hits);
+/* closest-hit rays with the ordered rule (closest_hit_ordered), hits as hko_trace */
+void hko_trace_ordered(hko_ctx* ctx, const float* rays, uint32_t n, void* hits);
 
 /* building blocks exposed for known-answer tests */
 float hko_intersects_aabb(const float* origin, const float* inv_dir, const float* mn, const float* mx);

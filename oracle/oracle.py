@@ -44,7 +44,10 @@ def lib() -> C.CDLL:
         "hko_reservoirs": (vp, [vp, C.c_int, C.POINTER(u32)]),
         "hko_counters": (None, [vp, vp]),
         "hko_reset_counters": (None, [vp]),
+        "hko_set_light_walk": (None, [vp, C.c_int]),
+        "hko_light_walk_stats": (None, [vp, vp]),
         "hko_trace": (None, [vp, vp, vp, vp, vp, u32, vp]),
+        "hko_trace_ordered": (None, [vp, vp, u32, vp]),
         "hko_primary_hits": (None, [vp, vp, vp]),
         "hko_intersects_aabb": (f, [vp, vp, vp, vp]),
         "hko_intersects_triangle": (None, [vp, vp, vp, vp, vp, vp]),
@@ -86,8 +89,13 @@ def default_threads() -> int:
 class Oracle:
     """CPU restatement of one camera's integrator state (same API shape as HikariRenderer)."""
 
+    WALK_REFERENCE, WALK_ORDERED, WALK_CHECK = 0, 1, 2
+
     def __init__(self, scene_desc, noise: np.ndarray, width: int, height: int, ratio: float = 1.0, threads: int = 0,
-                 textures=None):
+                 textures=None, light_walk: int = 0):
+        """light_walk (analysis, tests/test_light_walks.py): the closest-hit light walks in light.wgsl's order (0, the
+        restatement), the bounce walk with the ordered rule (1), or light.wgsl's order with every bounce ray also
+        walked with the ordered rule and render_frame raising if any ray's two results differ (2, WALK_CHECK)."""
         L = lib()
         self._L = L
         self._noise = np.ascontiguousarray(noise, np.uint8)
@@ -96,6 +104,8 @@ class Oracle:
         self.width, self.height = width, height
         if textures:
             self.set_textures(textures)
+        self.light_walk = int(light_walk)
+        L.hko_set_light_walk(self.ctx, self.light_walk)
 
     def set_textures(self, textures):
         """Material textures (a list of hikari_amd.Texture), as hk_texture_upload."""
@@ -137,6 +147,10 @@ class Oracle:
 
     def render_frame(self, settings, inputs):
         self._L.hko_render_frame(self.ctx, C.byref(settings), C.byref(inputs))
+        if self.light_walk == self.WALK_CHECK:
+            st = self.light_walk_stats()
+            if st["bounce_differ"]:
+                raise AssertionError(f"the ordered bounce walk differs from light.wgsl's order: {st}")
 
     def denoise(self, settings, inputs):
         self._L.hko_denoise(self.ctx, C.byref(settings), C.byref(inputs))
@@ -175,11 +189,29 @@ class Oracle:
     def reset_counters(self):
         self._L.hko_reset_counters(self.ctx)
 
+    def set_light_walk(self, mode: int):
+        """The closest-hit light walks: light.wgsl's order (0), the bounce walk with the ordered rule (1), or light.wgsl's
+        order with every bounce and emitter walk also walked with the ordered rule and the differing rays counted (2)."""
+        self.light_walk = int(mode)
+        self._L.hko_set_light_walk(self.ctx, self.light_walk)
+
+    def light_walk_stats(self) -> dict:
+        v = (C.c_uint64 * 4)()
+        self._L.hko_light_walk_stats(self.ctx, v)
+        return {"bounce_checked": v[0], "bounce_differ": v[1], "emitter_checked": v[2], "emitter_differ": v[3]}
+
     def primary_hits(self, frame_inputs) -> np.ndarray:
         """(h, w, 2, 3) words: [ordered walk, reference-order walk] x (instance, primitive, distance bits)."""
         out = np.empty((self.height, self.width, 2, 3), np.uint32)
         self._L.hko_primary_hits(self.ctx, C.byref(frame_inputs), out.ctypes.data)
         return out
+
+    def trace_ordered(self, rays) -> np.ndarray:
+        """Closest-hit rays with the ordered rule; hits as trace()."""
+        rays = np.ascontiguousarray(rays, np.float32)
+        hits = np.empty((len(rays), 5), np.uint32)
+        self._L.hko_trace_ordered(self.ctx, rays.ctypes.data, len(rays), hits.ctypes.data)
+        return hits
 
     def trace(self, rays, max_distance=None, early_distance=None, exclude=None) -> np.ndarray:
         rays = np.ascontiguousarray(rays, np.float32)

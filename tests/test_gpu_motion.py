@@ -291,9 +291,9 @@ def test_host_gbuffer_planes_bit_exact():
 def test_forced_kernel_variants_bit_exact(hk_options, lds):
     """Kernel variants the size thresholds normally pick only at large sizes, forced on a small
     frame: k_direct_lit_w4 (4 waves per SIMD; direct_w4_min_px=0 with fuse=0), the fused
-    direct+emissive launch next to the indirect side stream (fuse_min_px=0, merge=0; its emitter walks
-    compacted per workgroup, and with compact_emitter=0 per pixel, with compact_shadow=1 its shadow walks
-    compacted too) and the
+    direct+emissive launch next to the indirect side stream (fuse_min_px=0, merge=0: its emitter walks per
+    pixel; with compact_emitter=1 compacted per workgroup, k_direct_fused_cw<VD, false>; with compact_shadow=1
+    its shadow walks and the indirect pass's compacted too, k_direct_fused_cw<VD, true>) and the
     merged direct+indirect launch (k_light_merged, merge=1: the default only for small frames without
     spatial reuse; here with spatial reuse after it) and the persistent-wave indirect pass
     (k_indirect_persist, persistent_indirect=1, an opt-in), each with and without LDS scene staging."""
@@ -303,7 +303,7 @@ def test_forced_kernel_variants_bit_exact(hk_options, lds):
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
     s = st.to_c()
     for env in ({"direct_w4_min_px": 0, "fuse": 0}, {"fuse_min_px": 0, "merge": 0},
-                {"fuse_min_px": 0, "merge": 0, "compact_emitter": 0},
+                {"fuse_min_px": 0, "merge": 0, "compact_emitter": 1},
                 {"fuse_min_px": 0, "merge": 0, "compact_shadow": 1},
                 {"merge": 1}, {"persistent_indirect": 1, "merge": 0}):
         hk_options.clear()
