@@ -1943,9 +1943,21 @@ __global__ __launch_bounds__(256) void k_spatial_nowin(FrameArgs A, ChannelArgs 
 __constant__ float KERNEL3[3][3] = {{0.0625f, 0.125f, 0.0625f}, {0.125f, 0.25f, 0.125f}, {0.0625f, 0.125f, 0.0625f}};
 
 HKD bool uv_outside(f2 uv) { return uv.x < 0.0f || uv.y < 0.0f || uv.x > 1.0f || uv.y > 1.0f; }
+// NaN or +inf in a component (denoise.wgsl's `any(isnan) || any(x > F32_MAX)` skip): one class test per
+// component (v_cmp_class_f32: signalling / quiet NaN, +inf) instead of two compares
 HKD bool bad3(f3 v)
 {
-    return (v.x != v.x) || (v.y != v.y) || (v.z != v.z) || v.x > HK_F32_MAX || v.y > HK_F32_MAX || v.z > HK_F32_MAX;
+    constexpr int NAN_PINF = 0x1 | 0x2 | 0x200;
+    return __builtin_amdgcn_classf(v.x, NAN_PINF) || __builtin_amdgcn_classf(v.y, NAN_PINF) ||
+           __builtin_amdgcn_classf(v.z, NAN_PINF);
+}
+// plane index of an integrator pixel for the denoiser, which never runs on interleaved stripes (hk_denoise
+// rejects them): s_index without the stripe map
+HKD int32_t dn_index(const Frame& F, int32_t x, int32_t y)
+{
+    int32_t ly = y - F.s_row0;
+    ly = ly < 0 ? 0 : (ly >= F.s_rows ? F.s_rows - 1 : ly);
+    return x + (int32_t)F.s[0] * ly;
 }
 // albedo plane is S-sized (band-local rows)
 HKD f4 load_albedo(const Frame& F, const uint2* albedo, int32_t x, int32_t y)
@@ -1953,16 +1965,30 @@ HKD f4 load_albedo(const Frame& F, const uint2* albedo, int32_t x, int32_t y)
     return load_rgba16f(albedo, band_index(F, x, y, F.S[0], F.S_row0, F.S_rows));
 }
 
-// Channel-fused denoiser.  The reference runs demodulation + 4 levels separately for each
-// of the 3 channels (post_process.rs:1199-1223); channels are independent and share every
-// geometry weight, so one launch per level processes all channels and computes the normal /
-// depth / instance weights of each tap once.  The per-pixel geometry (normalised normal,
-// depth, instance, depth gradient at the pixel's deferred texel) is produced once per frame
-// by k_demod3 with exactly the expressions denoise.wgsl evaluates per tap.
-HKD void store_geom(const DenoiseArgs& D, int32_t idx, f3 n, float depth, float inst, f2 grad)
+// Channel-fused denoiser.  The reference runs demodulation + 4 levels separately for each of the 3 channels
+// (post_process.rs:1199-1223); channels are independent and share every geometry weight, so one launch per level
+// processes all channels and computes the normal / depth / instance weights of each tap once.  Demodulation
+// produces, with exactly the expressions denoise.wgsl evaluates per tap:
+//   nd      (normalised normal, depth) of the pixel's deferred texel          — read at every tap
+//   center  (depth gradient x, y, luminance denominator of channels 0, 1)     — read at the pixel only
+//   den2    (luminance denominator of channel 2)                                — read at the pixel only
+// and the level-0 input.  A level's input / output (the reference's internal textures, RGBA16F per channel)
+// is kept as the three channels' RGB halves packed into 20 bytes plus the pixel's instance (alpha is never
+// read): rgb[L] = r0 g0 | b0 r1 | g1 b1 | r2 g2, bi[L] = b2 | (instance bits); the halves are the f16 bits the
+// reference stores (pack2x16float), so every value read back is unchanged.  The planes are private to
+// hk_denoise (no output id reads them).
+HKD void store_level(const DenoiseArgs& D, int level, int32_t idx, f3 c0, f3 c1, f3 c2, uint32_t inst_bits)
 {
-    D.geom[2 * idx] = make_float4(n.x, n.y, n.z, depth);
-    D.geom[2 * idx + 1] = make_float4(inst, grad.x, grad.y, 0.0f);
+    D.rgb[level][idx] = make_uint4(pack2x16float(c0.x, c0.y), pack2x16float(c0.z, c1.x), pack2x16float(c1.y, c1.z),
+                                   pack2x16float(c2.x, c2.y));
+    D.bi[level][idx] = make_uint2(pack2x16float(c2.z, 0.0f), inst_bits);
+}
+// channel ch's RGB from a packed texel (ch: an unrolled loop's constant)
+HKD f3 dn_rgb(int ch, uint4 rgb, uint2 bi)
+{
+    if (ch == 0) return mk3(unpack_lo16float(rgb.x), unpack_hi16float(rgb.x), unpack_lo16float(rgb.y));
+    if (ch == 1) return mk3(unpack_hi16float(rgb.y), unpack_lo16float(rgb.z), unpack_hi16float(rgb.z));
+    return mk3(unpack_lo16float(rgb.w), unpack_hi16float(rgb.w), unpack_lo16float(bi.x));
 }
 
 template <int C>
@@ -1978,22 +2004,26 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
     nearest_texel(duv, F.S, ax, ay);
     // (ax, ay) is a nearest_texel: inside the frame, so the load_* bounds tests always pass; the texels are read
     // directly, without their branch regions, so all of them are in flight together (same texels, same values)
+    float inst;
+    float2 grad;
     {
         const int32_t g = band_index(F, ax, ay, F.S[0], F.S_row0, F.S_rows);
         const uint32_t n = A.G.normal[g];
-        const f3 normal = mk3(hk_unpack_snorm8_fast(n, 0), hk_unpack_snorm8_fast(n, 1), hk_unpack_snorm8_fast(n, 2));
-        const float2 grad = A.G.depth_gradient[g];
-        store_geom(D, idx, normalize(normal), A.G.position[g].w, A.G.instance_material[g].x, mk2(grad.x, grad.y));
+        const f3 normal = normalize(mk3(hk_unpack_snorm8_fast(n, 0), hk_unpack_snorm8_fast(n, 1), hk_unpack_snorm8_fast(n, 2)));
+        D.nd[idx] = make_float4(normal.x, normal.y, normal.z, A.G.position[g].w);  // denoise.wgsl:220-223, 197-200
+        grad = A.G.depth_gradient[g];
+        inst = A.G.instance_material[g].x;
     }
     f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
     nearest_texel(uv, F.s, rx, ry);
     const int32_t ridx = s_index(F, rx, ry);
+    f3 out[3] = {mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0)};
+    float den[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) {
         f3 irr = xyz(load_rgba16f(D.render[ch], ridx));
-        irr = mk3(albedo.x < 0.01f ? 0.0f : irr.x / albedo.x, albedo.y < 0.01f ? 0.0f : irr.y / albedo.y,
-                  albedo.z < 0.01f ? 0.0f : irr.z / albedo.z);
-        store_rgba16f(D.internal[ch][0], idx, mk4(irr.x, irr.y, irr.z, 1.0f));
+        out[ch] = mk3(albedo.x < 0.01f ? 0.0f : irr.x / albedo.x, albedo.y < 0.01f ? 0.0f : irr.y / albedo.y,
+                      albedo.z < 0.01f ? 0.0f : irr.z / albedo.z);
         float sum_variance = 0.0f;
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
@@ -2007,33 +2037,84 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
             sum_variance = (uv_outside(suv) || v > HK_F32_MAX) ? sum_variance : t;
         }
         D.internal_variance[ch][idx] = sum_variance;
+        // the levels' luminance-weight denominator (denoise.wgsl:56-60: strictness 4, exponent 0.25, eps 0.001) of
+        // this pixel's variance, the same in every level: evaluated once here instead of once per level
+        den[ch] = 4.0f * hk_pow(sum_variance, 0.25f) + 0.001f;
     }
+    // internal0 = (irradiance / albedo, 1) per channel (denoise.wgsl:143-147), packed
+    store_level(D, 0, idx, out[0], out[1], out[2], __float_as_uint(inst));
+    D.center[idx] = make_float4(grad.x, grad.y, den[0], den[1]);
+    if (C == 3) D.den2[idx] = den[2];
 }
 
+// One a-trous level (denoise.wgsl:215-319) with its inputs staged in LDS.  A workgroup's 16x16 tile reads its taps
+// from the tile grown by the level's step on every side ((16 + 2 step)^2 texels: 4x the tile at step 8, 1.27x at
+// step 1); the workgroup copies that region once — each texel's (normal, depth), packed channels and instance,
+// three coalesced 16 / 16 / 8-byte loads — and the taps then read LDS instead of gathering ~37 scattered texels
+// per pixel through the caches.  Every value is the one a per-tap load would read (dn_index of the same
+// coordinates) and the arithmetic per tap is the reference's, so the stored bits are those of the per-tap
+// version: city 4K 0.417 -> 0.354 ms per level (profiles/r05/c3).  Row stride: an odd multiple of 8 texels, so the
+// two 8-texel rows of a 16-lane LDS read phase fall in different halves of the banks.
+template <int LEVEL>
+struct DnRegion {
+    static constexpr int32_t step = 8 >> LEVEL;
+    static constexpr int32_t W = 16 + 2 * step;                        // region width = height
+    static constexpr int32_t STRIDE = (W % 16 == 8) ? W : (W / 16) * 16 + (W % 16 < 8 ? 8 : 24);
+    static constexpr int32_t N = W * STRIDE;
+};
 template <int C, int LEVEL>
 __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
+    using R = DnRegion<LEVEL>;
+    constexpr int32_t step = R::step;
+    __shared__ float4 s_nd[R::N];
+    __shared__ uint4 s_rgb[R::N];
+    __shared__ uint2 s_bi[R::N];
     const Frame& F = A.F;
+    int32_t x0, y0;
+    tile_origin<DENOISE_ORDER>(F, F.s_row0, x0, y0);
+    {
+        const int32_t rx0 = x0 - step, ry0 = y0 - step;
+        for (int32_t k = (int32_t)threadIdx.x; k < R::W * R::W; k += 256) {
+            const int32_t ry = k / R::W, rx = k - ry * R::W;
+            // out-of-frame texels are never tapped (the tap bounds test below); read at clamped coordinates
+            const int32_t sidx = dn_index(F, min(max(rx0 + rx, 0), (int32_t)F.s[0] - 1), min(max(ry0 + ry, 0), (int32_t)F.s[1] - 1));
+            const float4 nd = D.nd[sidx];
+            const uint4 rgb = D.rgb[LEVEL][sidx];
+            const uint2 bi = D.bi[LEVEL][sidx];
+            const int32_t o = ry * R::STRIDE + rx;
+            s_nd[o] = nd;
+            s_rgb[o] = rgb;
+            s_bi[o] = bi;
+        }
+    }
+    __syncthreads();
     int32_t x, y;
     if (!tile_pixel<DENOISE_ORDER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
-    const int32_t idx = s_index(F, x, y);
-    constexpr int32_t step = 8 >> LEVEL;
-    const float4 g0 = D.geom[2 * idx], g1 = D.geom[2 * idx + 1];
+    const int32_t idx = dn_index(F, x, y);
+    const int32_t oc = (y - y0 + step) * R::STRIDE + (x - x0 + step);  // the pixel in the region
+    const float4 g0 = s_nd[oc];
+    const uint2 cbi = s_bi[oc];
     const float depth = g0.w;
     if (depth < HK_F32_EPSILON) {
+        if (LEVEL == 3) {
 #pragma unroll
-        for (int ch = 0; ch < C; ++ch) store_rgba16f(LEVEL == 3 ? D.output[ch] : D.internal[ch][LEVEL + 1], idx, mk4(0, 0, 0, 0));
+            for (int ch = 0; ch < C; ++ch) store_rgba16f(D.output[ch], idx, mk4(0, 0, 0, 0));
+        } else {
+            store_level(D, LEVEL + 1, idx, mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0), cbi.y);
+        }
         return;
     }
+    const float4 gc = D.center[idx];
     const f3 normal = mk3(g0.x, g0.y, g0.z);
-    const float instance = g1.x;
-    const f2 depth_gradient = mk2(g1.y, g1.z);
+    const float instance = __uint_as_float(cbi.y);
+    const f2 depth_gradient = mk2(gc.x, gc.y);
     f3 sum_irr[C], irradiance[C];
     float sum_w[C], l0[C], lum_denom[C], lum_rcp[C], m1[C], m2[C], cnt[C];
+    const uint4 crgb = s_rgb[oc];
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) {
-        float variance = D.internal_variance[ch][idx];
-        irradiance[ch] = xyz(load_rgba16f(D.internal[ch][LEVEL], idx));
+        irradiance[ch] = dn_rgb(ch, crgb, cbi);
         sum_irr[ch] = irradiance[ch] * 0.25f;
         sum_w[ch] = 0.25f;
         if (bad3(irradiance[ch])) {
@@ -2042,72 +2123,10 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
             sum_w[ch] = 0.0f;
         }
         l0[ch] = lum(irradiance[ch]);
-        lum_denom[ch] = 4.0f * hk_pow(variance, 0.25f) + 0.001f;
-        lum_rcp[ch] = 1.0f / lum_denom[ch];
+        lum_denom[ch] = ch == 0 ? gc.z : (ch == 1 ? gc.w : D.den2[idx]);  // k_demod3
+        lum_rcp[ch] = rcp_exact(lum_denom[ch]);                           // == 1 / lum_denom (all inputs)
         m1[ch] = m2[ch] = cnt[ch] = 0.0f;
     }
-#if HK_DENOISE_PF
-    // The taps in two batches of four: every texel of a batch read first (out-of-frame taps at clamped coordinates,
-    // their values unused), then the batch's taps evaluated exactly as below, branches included.  The empty asm
-    // statement takes the batch's values, so all of its loads are issued before the first is waited for.
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        float4 t0s[4];
-        float sis[4];
-        uint2 irs[4][C];
-        int32_t sxs[4], sys[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k = 4 * b + j;
-            const int kk = k < 4 ? k : k + 1;
-            const int ox = kk % 3 - 1, oy = kk / 3 - 1;
-            sxs[j] = x + ox * step;
-            sys[j] = y + oy * step;
-            const int32_t sidx = s_index(F, min(max(sxs[j], 0), (int32_t)F.s[0] - 1), min(max(sys[j], 0), (int32_t)F.s[1] - 1));
-            t0s[j] = D.geom[2 * sidx];
-            sis[j] = D.geom[2 * sidx + 1].x;
-#pragma unroll
-            for (int ch = 0; ch < C; ++ch) irs[j][ch] = D.internal[ch][LEVEL][sidx];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            __asm__ volatile("" ::"v"(t0s[j].x), "v"(t0s[j].y), "v"(t0s[j].z), "v"(t0s[j].w), "v"(sis[j]));
-#pragma unroll
-            for (int ch = 0; ch < C; ++ch) __asm__ volatile("" ::"v"(irs[j][ch].x), "v"(irs[j][ch].y));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k = 4 * b + j;
-            const int kk = k < 4 ? k : k + 1;
-            const int ox = kk % 3 - 1, oy = kk / 3 - 1;
-            const int32_t sx = sxs[j], sy = sys[j];
-            if (sx < 0 || sy < 0 || sx >= (int32_t)F.s[0] || sy >= (int32_t)F.s[1]) continue;
-            const float4 t0 = t0s[j];
-            const float si = sis[j];
-            const float w_normal = hk_pow16(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))));
-            const float w_depth = hk_exp((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
-            const float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
-            const float w_geo = (w_normal * w_depth) * w_instance;
-            const float kw = KERNEL3[oy + 1][ox + 1];
-#pragma unroll
-            for (int ch = 0; ch < C; ++ch) {
-                const uint2 v = irs[j][ch];
-                f3 irr = mk3(unpack_lo16float(v.x), unpack_hi16float(v.x), unpack_lo16float(v.y));
-                if (bad3(irr)) continue;
-                float sl = lum(irr);
-                float w_lum = hk_exp(div_by(-fabsf(l0[ch] - sl), lum_denom[ch], lum_rcp[ch]));
-                float w = hk_clampf(w_geo * w_lum, 0.0f, 1.0f) * kw;
-                sum_irr[ch] = sum_irr[ch] + irr * w;
-                sum_w[ch] += w;
-                if (ch >= 1) {
-                    m1[ch] += sl;
-                    m2[ch] += sl * sl;
-                    cnt[ch] += 1.0f;
-                }
-            }
-        }
-    }
-#else
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int kk = k < 4 ? k : k + 1;  // skip the centre
@@ -2116,9 +2135,11 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         // uv_outside(coords_to_uv(s)) exactly: (sx + 0.5) / w < 0 iff sx < 0, and its rounding
         // exceeds 1 iff sx >= w (for w < 2^24 the quotient is >= 1 + 2^-13 or <= 1 - 2^-25)
         if (sx < 0 || sy < 0 || sx >= (int32_t)F.s[0] || sy >= (int32_t)F.s[1]) continue;
-        const int32_t sidx = s_index(F, sx, sy);
-        const float4 t0 = D.geom[2 * sidx];
-        const float si = D.geom[2 * sidx + 1].x;
+        const int32_t o = oc + oy * step * R::STRIDE + ox * step;
+        const float4 t0 = s_nd[o];
+        const uint4 trgb = s_rgb[o];
+        const uint2 tbi = s_bi[o];
+        const float si = __uint_as_float(tbi.y);
         const float w_normal = hk_pow16(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))));
         const float w_depth = hk_exp((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
         const float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
@@ -2126,7 +2147,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         const float kw = KERNEL3[oy + 1][ox + 1];
 #pragma unroll
         for (int ch = 0; ch < C; ++ch) {
-            f3 irr = xyz(load_rgba16f(D.internal[ch][LEVEL], sidx));
+            f3 irr = dn_rgb(ch, trgb, tbi);
             if (bad3(irr)) continue;
             float sl = lum(irr);
             // x / lum_denom with the per-pixel reciprocal (div_by: the IEEE quotient for normal
@@ -2143,13 +2164,13 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
             }
         }
     }
-#endif
     f4 a = mk4(0, 0, 0, 0);
     if (LEVEL == 3) {
         int32_t gx, gy;
         nearest_texel(jittered_uv(F, coords_to_uv(x, y, F.s), 0.5f), F.S, gx, gy);
         a = load_albedo(F, D.albedo, gx, gy);
     }
+    f3 res[3] = {mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0)};
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) {
         f3 ir = sum_w[ch] < 0.0001f ? mk3(0, 0, 0) : sum_irr[ch] / sum_w[ch];
@@ -2158,10 +2179,12 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
             float var = m2[ch] / cnt[ch] - mean * mean;
             if (l0[ch] > mean + 3.0f * sqrtf(var)) ir = ir * (mean / l0[ch]);
         }
-        f4 color = mk4(ir.x, ir.y, ir.z, 1.0f);
-        if (LEVEL == 3) color = mk4(color.x * a.x, color.y * a.y, color.z * a.z, color.w * a.w);
-        store_rgba16f(LEVEL == 3 ? D.output[ch] : D.internal[ch][LEVEL + 1], idx, color);
+        if (LEVEL == 3) {  // the output texture: (ir, 1) x albedo
+            store_rgba16f(D.output[ch], idx, mk4(ir.x * a.x, ir.y * a.y, ir.z * a.z, 1.0f * a.w));
+        }
+        res[ch] = ir;
     }
+    if (LEVEL < 3) store_level(D, LEVEL + 1, idx, res[0], res[1], res[2], cbi.y);
 }
 
 // ------------------------------------------------------------------ tone mapping (tone_mapping.wgsl:21-32)

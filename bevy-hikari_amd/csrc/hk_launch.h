@@ -99,10 +99,15 @@ struct DenoiseArgs {
     const uint2* albedo;     // S
     const uint2* render[3];  // s
     const float* variance[3];
-    uint2* internal[3][4];
+    // a level's input (the reference's internal textures of the 3 channels, hk_kernels.hip store_level): RGB f16
+    // halves packed r0 g0 | b0 r1 | g1 b1 | r2 g2, and b2 | instance bits
+    uint4* rgb[4];
+    uint2* bi[4];
     float* internal_variance[3];
     uint2* output[3];
-    float4* geom;            // 2 x float4 per pixel: (normal, depth), (instance, depth gradient)
+    float4* nd;              // per pixel: (normalised normal, depth)
+    float4* center;          // per pixel: (depth gradient x, y, luminance denominator of channels 0, 1)
+    float* den2;             // per pixel: luminance denominator of channel 2
 };
 
 struct ToneArgs {

@@ -3,7 +3,7 @@
 // One hk_ctx per camera entity owns everything the reference keeps per view:
 //   ReservoirCache (light.rs:342-363)        -> 10 SoA reservoir buffers in HBM
 //   LightTextures (light.rs:297-383)          -> albedo (S), variance[3], render[3] (s)
-//   PostProcessTextures denoise part (post_process.rs:710-714) -> internal[4], internal variance,
+//   PostProcessTextures denoise part (post_process.rs:710-714) -> internal[4] (packed: dn_rgb / dn_bi), internal variance,
 //                                               denoised[3], tone-mapped output
 //   group-2 scene buffers (mesh_material/mod.rs:488-598) -> device copies of the std430 arrays
 // hk_render_frame issues the kernels in LightNode::run order (light.rs:646-699) and
@@ -195,9 +195,12 @@ struct hk_ctx {
     bool gb_valid = false;
     int32_t gb_key[2] = {};
     // denoise
-    uint2* internal[3][4] = {};
+    uint4* dn_rgb[4] = {};        // a-trous level inputs, the 3 channels packed (DenoiseArgs::rgb / bi)
+    uint2* dn_bi[4] = {};
     float* internal_variance[3] = {};
-    float4* geom = nullptr;
+    float4* dn_nd = nullptr;      // (normal, depth) per pixel (k_demod3)
+    float4* dn_center = nullptr;  // (depth gradient, luminance denominators of channels 0, 1) per pixel
+    float* dn_den2 = nullptr;     // luminance denominator of channel 2 per pixel
     int last_denoised_channels = 3;
     uint2* denoised[3] = {};
     uint2* tone_buf[2] = {};      // tone_mapping_output[2], written at [head]
@@ -395,10 +398,15 @@ void free_targets(hk_ctx* c)
     c->gb_valid = false;
     release(c->sp_view);
     for (int ch = 0; ch < 3; ++ch) {
-        for (int i = 0; i < 4; ++i) release(c->internal[ch][i]);
         release(c->internal_variance[ch]);
     }
-    release(c->geom);
+    for (int i = 0; i < 4; ++i) {
+        release(c->dn_rgb[i]);
+        release(c->dn_bi[i]);
+    }
+    release(c->dn_nd);
+    release(c->dn_center);
+    release(c->dn_den2);
     for (int k = 0; k < 2; ++k) {
         release(c->tone_buf[k]);
         release(c->taa_buf[k]);
@@ -1229,15 +1237,21 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     HK_HIP(c, hipMalloc(&c->sp_view, VIEW_PLANES * sp * sizeof(uint4)));
     HK_HIP(c, hipMemset(c->sp_view, 0, VIEW_PLANES * sp * sizeof(uint4)));
     for (int ch = 0; ch < 3; ++ch) {
-        for (int i = 0; i < 4; ++i) {
-            HK_HIP(c, hipMalloc(&c->internal[ch][i], sp * sizeof(uint2)));
-            HK_HIP(c, hipMemset(c->internal[ch][i], 0, sp * sizeof(uint2)));
-        }
         HK_HIP(c, hipMalloc(&c->internal_variance[ch], sp * sizeof(float)));
         HK_HIP(c, hipMemset(c->internal_variance[ch], 0, sp * sizeof(float)));
     }
-    HK_HIP(c, hipMalloc(&c->geom, 2 * sp * sizeof(float4)));
-    HK_HIP(c, hipMemset(c->geom, 0, 2 * sp * sizeof(float4)));
+    for (int i = 0; i < 4; ++i) {
+        HK_HIP(c, hipMalloc(&c->dn_rgb[i], sp * sizeof(uint4)));
+        HK_HIP(c, hipMemset(c->dn_rgb[i], 0, sp * sizeof(uint4)));
+        HK_HIP(c, hipMalloc(&c->dn_bi[i], sp * sizeof(uint2)));
+        HK_HIP(c, hipMemset(c->dn_bi[i], 0, sp * sizeof(uint2)));
+    }
+    HK_HIP(c, hipMalloc(&c->dn_nd, sp * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->dn_nd, 0, sp * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->dn_center, sp * sizeof(float4)));
+    HK_HIP(c, hipMemset(c->dn_center, 0, sp * sizeof(float4)));
+    HK_HIP(c, hipMalloc(&c->dn_den2, sp * sizeof(float)));
+    HK_HIP(c, hipMemset(c->dn_den2, 0, sp * sizeof(float)));
     for (int k = 0; k < 2; ++k) {
         HK_HIP(c, hipMalloc(&c->tone_buf[k], sp * sizeof(uint2)));
         HK_HIP(c, hipMemset(c->tone_buf[k], 0, sp * sizeof(uint2)));
@@ -1747,11 +1761,16 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     for (int ch = 0; ch < 3; ++ch) {
         D.render[ch] = c->render[ch];
         D.variance[ch] = c->variance[ch];
-        for (int i = 0; i < 4; ++i) D.internal[ch][i] = c->internal[ch][i];
         D.internal_variance[ch] = c->internal_variance[ch];
         D.output[ch] = c->denoised[ch];
     }
-    D.geom = c->geom;
+    for (int i = 0; i < 4; ++i) {
+        D.rgb[i] = c->dn_rgb[i];
+        D.bi[i] = c->dn_bi[i];
+    }
+    D.nd = c->dn_nd;
+    D.center = c->dn_center;
+    D.den2 = c->dn_den2;
     c->last_denoised_channels = channels;
     // band windows (pass_window): demodulation on core +-15, the levels on +-7, 3, 1, 0
     const FrameArgs AD = pass_window(c, A, DENOISE_OUT_REACH - 1);

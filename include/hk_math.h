@@ -45,12 +45,14 @@ HK_HD float hk_absf(float x) { return hk_u2f(hk_f2u(x) & 0x7FFFFFFFu); }
 HK_HD float hk_signf(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 HK_HD float hk_mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
 
-/* 2^x.  Range-reduce to n + f, |f| <= 0.5; degree-7 Taylor of e^(f ln2) in Horner form. */
+/* 2^x.  Range-reduce to n + f, |f| <= 0.5; degree-7 Taylor of e^(f ln2) in Horner form.
+ * Written without branches: every case's value is computed and the result selected at the end
+ * (x NaN -> x; x >= 128 -> +inf; x < -151 -> 0; n >= -126 -> p * 2^n; else the subnormal result in
+ * two exact-exponent steps, the last one rounding once).  The same bits as the branchy form for all
+ * 2^32 inputs (oracle hko_math_form_mismatches, tests/test_oracle_kat.py); on the GPU a wave then runs
+ * one straight sequence instead of three exec-mask regions per call (35 calls per a-trous pixel). */
 HK_HD float hk_exp2(float x)
 {
-    if (x != x) return x;
-    if (x >= 128.0f) return hk_u2f(0x7F800000u);
-    if (x < -151.0f) return 0.0f;
     float n = rintf(x);
     float f = x - n;
     float p = 1.5252733804059840e-05f;        /* ln2^7/7! */
@@ -61,29 +63,32 @@ HK_HD float hk_exp2(float x)
     p = p * f + 2.4022650695910071e-01f;      /* ln2^2/2! */
     p = p * f + 6.9314718055994531e-01f;      /* ln2 */
     p = p * f + 1.0f;
-    int32_t ni = (int32_t)n;
-    if (ni >= -126) {
-        return p * hk_u2f((uint32_t)(ni + 127) << 23);
-    }
-    /* subnormal result: two exact-exponent steps, the last one rounds once */
-    return (p * hk_u2f((uint32_t)(ni + 64 + 127) << 23)) * hk_u2f((uint32_t)(-64 + 127) << 23);
+    /* n clamped before the conversion (only the selected cases use it: -151 <= n <= 128) */
+    const int32_t ni = (int32_t)hk_minf(hk_maxf(n, -160.0f), 160.0f);
+    const int normal = ni >= -126;
+    const float s1 = hk_u2f((uint32_t)(normal ? ni + 127 : ni + 64 + 127) << 23);
+    const float s2 = normal ? 1.0f : hk_u2f((uint32_t)(-64 + 127) << 23);
+    float r = (p * s1) * s2; /* x 1.0 is exact */
+    r = x < -151.0f ? 0.0f : r;
+    r = x >= 128.0f ? hk_u2f(0x7F800000u) : r;
+    return x != x ? x : r;
 }
 
 HK_HD float hk_exp(float x) { return hk_exp2(x * 1.4426950408889634f); }
 
-/* log2(x): x = m * 2^e with m in [sqrt(1/2), sqrt(2)); log2(m) via atanh series of s=(m-1)/(m+1). */
+/* log2(x): x = m * 2^e with m in [sqrt(1/2), sqrt(2)); log2(m) via atanh series of s=(m-1)/(m+1).
+ * Branch-free like hk_exp2 (x NaN -> x; x < 0 -> NaN; x == 0 -> -inf; x == +inf -> +inf; subnormal
+ * x normalised first); the same bits as the branchy form for all 2^32 inputs. */
 HK_HD float hk_log2(float x)
 {
-    if (x != x) return x;
-    if (x < 0.0f) return hk_u2f(0x7FC00000u);
-    if (x == 0.0f) return hk_u2f(0xFF800000u);
-    if (x == hk_u2f(0x7F800000u)) return x;
-    int32_t e = 0;
-    if (x < 1.17549435e-38f) { x = x * 8388608.0f; e = -23; } /* normalize subnormals */
-    uint32_t u = hk_f2u(x);
-    e += (int32_t)((u >> 23) & 0xFF) - 127;
+    const int sub = x < 1.17549435e-38f; /* normalize subnormals (x <= 0 and NaN are selected away below) */
+    const float xn = sub ? x * 8388608.0f : x;
+    const uint32_t u = hk_f2u(xn);
+    int32_t e = (sub ? -23 : 0) + (int32_t)((u >> 23) & 0xFF) - 127;
     float m = hk_u2f((u & 0x007FFFFFu) | 0x3F800000u); /* [1,2) */
-    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    const int big = m > 1.41421356f;
+    m = big ? m * 0.5f : m;
+    e += big ? 1 : 0;
     float s = (m - 1.0f) / (m + 1.0f);
     float s2 = s * s;
     float p = 0.11111111111111111f;          /* 1/9 */
@@ -92,7 +97,11 @@ HK_HD float hk_log2(float x)
     p = p * s2 + 0.33333333333333333f;       /* 1/3 */
     p = p * s2 + 1.0f;
     float lm = (p * s) * 2.8853900817779268f; /* 2/ln2 */
-    return (float)e + lm;
+    float r = (float)e + lm;
+    r = x == hk_u2f(0x7F800000u) ? x : r;
+    r = x == 0.0f ? hk_u2f(0xFF800000u) : r;
+    r = x < 0.0f ? hk_u2f(0x7FC00000u) : r;
+    return x != x ? x : r;
 }
 
 /* WGSL pow(x, y) = exp2(y * log2(x)) for x >= 0 (NaN for x < 0). */

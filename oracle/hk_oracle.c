@@ -2533,6 +2533,63 @@ uint32_t hko_unpack_fast_mismatches(void)
     }
     return bad;
 }
+/* The branchy forms hk_math.h's hk_exp2 / hk_log2 had through round 4 (branch-free since round 5): the
+ * count of inputs, over every stride-th of the 2^32 bit patterns (stride 1: all of them, ~50 s on 8
+ * cores; 0 and 0 when last run), where the current form's bits differ from these (NaN payloads included) */
+static float exp2_branchy(float x)
+{
+    if (x != x) return x;
+    if (x >= 128.0f) return hk_u2f(0x7F800000u);
+    if (x < -151.0f) return 0.0f;
+    float n = rintf(x);
+    float f = x - n;
+    float p = 1.5252733804059840e-05f;
+    p = p * f + 1.5403530393381608e-04f;
+    p = p * f + 1.3333558146428443e-03f;
+    p = p * f + 9.6181291076284772e-03f;
+    p = p * f + 5.5504108664821580e-02f;
+    p = p * f + 2.4022650695910071e-01f;
+    p = p * f + 6.9314718055994531e-01f;
+    p = p * f + 1.0f;
+    int32_t ni = (int32_t)n;
+    if (ni >= -126) return p * hk_u2f((uint32_t)(ni + 127) << 23);
+    return (p * hk_u2f((uint32_t)(ni + 64 + 127) << 23)) * hk_u2f((uint32_t)(-64 + 127) << 23);
+}
+static float log2_branchy(float x)
+{
+    if (x != x) return x;
+    if (x < 0.0f) return hk_u2f(0x7FC00000u);
+    if (x == 0.0f) return hk_u2f(0xFF800000u);
+    if (x == hk_u2f(0x7F800000u)) return x;
+    int32_t e = 0;
+    if (x < 1.17549435e-38f) { x = x * 8388608.0f; e = -23; }
+    uint32_t u = hk_f2u(x);
+    e += (int32_t)((u >> 23) & 0xFF) - 127;
+    float m = hk_u2f((u & 0x007FFFFFu) | 0x3F800000u);
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    float s = (m - 1.0f) / (m + 1.0f);
+    float s2 = s * s;
+    float p = 0.11111111111111111f;
+    p = p * s2 + 0.14285714285714285f;
+    p = p * s2 + 0.2f;
+    p = p * s2 + 0.33333333333333333f;
+    p = p * s2 + 1.0f;
+    float lm = (p * s) * 2.8853900817779268f;
+    return (float)e + lm;
+}
+void hko_math_form_mismatches(uint32_t stride, unsigned long long* out)
+{
+    unsigned long long be = 0, bl = 0;
+    const long long n = ((1ll << 32) + stride - 1) / stride;
+#pragma omp parallel for schedule(static) reduction(+ : be, bl)
+    for (long long k = 0; k < n; ++k) {
+        const float x = hk_u2f((uint32_t)(k * (long long)stride));
+        if (hk_f2u(hk_exp2(x)) != hk_f2u(exp2_branchy(x))) ++be;
+        if (hk_f2u(hk_log2(x)) != hk_f2u(log2_branchy(x))) ++bl;
+    }
+    out[0] = be;
+    out[1] = bl;
+}
 float hko_pow(float x, float y) { return hk_pow(x, y); }
 float hko_pow_int(float x, int n) { return n == 2 ? hk_pow2(x) : (n == 5 ? hk_pow5(x) : hk_pow16(x)); }
 float hko_exp2(float x) { return hk_exp2(x); }

@@ -77,6 +77,9 @@ void hko_pack_reservoir_roundtrip(const float* fields, hk_packed_reservoir* pack
 float hko_pow(float x, float y);
 float hko_pow_int(float x, int n); /* n in {2, 5, 16} */
 float hko_exp2(float x);
+/* [exp2, log2]: inputs (every stride-th of the 2^32) where hk_math.h's branch-free forms differ from the round-4
+ * branchy ones */
+void hko_math_form_mismatches(uint32_t stride, unsigned long long* out);
 float hko_log2(float x);
 float hko_sin(float x);
 float hko_cos(float x);

@@ -55,6 +55,7 @@ def lib() -> C.CDLL:
         "hko_pow": (f, [f, f]),
         "hko_pow_int": (f, [f, C.c_int]),
         "hko_exp2": (f, [f]),
+        "hko_math_form_mismatches": (None, [u32, vp]),
         "hko_log2": (f, [f]),
         "hko_sin": (f, [f]),
         "hko_cos": (f, [f]),

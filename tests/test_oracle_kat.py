@@ -213,6 +213,21 @@ def test_transcendentals_accuracy(oracle_lib, name, fn, lo, hi):
     assert worst <= 4.0, f"{name}: {worst} ulp"
 
 
+def test_branch_free_exp2_log2_equal_the_branchy_forms(oracle_lib):
+    """hk_math.h's hk_exp2 / hk_log2 are written branch-free since round 5 (each case computed, the result
+    selected); they must give the bits of the round-4 branchy forms (kept in the oracle as the reference) on
+    every input.  Every 7th of the 2^32 bit patterns here (all of them: 0 / 0 when run with stride 1)."""
+    import ctypes as C
+    v = (C.c_uint64 * 2)()
+    oracle_lib.hko_math_form_mismatches(7, v)
+    assert list(v) == [0, 0], list(v)
+    # the selected special cases
+    assert math.isnan(oracle_lib.hko_exp2(float("nan"))) and math.isnan(oracle_lib.hko_log2(-1.0))
+    assert oracle_lib.hko_exp2(128.0) == float("inf") and oracle_lib.hko_exp2(-151.5) == 0.0
+    assert oracle_lib.hko_exp2(-149.0) == 2.0 ** -149 and oracle_lib.hko_log2(0.0) == -float("inf")
+    assert oracle_lib.hko_log2(float("inf")) == float("inf") and oracle_lib.hko_log2(2.0 ** -140) == -140.0
+
+
 def test_pow_special_cases(oracle_lib):
     assert oracle_lib.hko_pow(0.0, 5.0) == 0.0
     assert oracle_lib.hko_pow(0.0, 0.25) == 0.0
