@@ -2141,7 +2141,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         const uint2 tbi = s_bi[o];
         const float si = __uint_as_float(tbi.y);
         const float w_normal = hk_pow16(fmaxf(0.0f, dot(normal, mk3(t0.x, t0.y, t0.z))));
-        const float w_depth = hk_exp((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
+        const float w_depth = hk_exp_weight((-fabsf(depth - t0.w)) / (fabsf(dot(depth_gradient, mk2((float)ox, (float)oy))) + 0.01f));
         const float w_instance = fmaxf(0.0f, 1.0f - fabsf(instance - si));
         const float w_geo = (w_normal * w_depth) * w_instance;
         const float kw = KERNEL3[oy + 1][ox + 1];
@@ -2152,8 +2152,9 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
             float sl = lum(irr);
             // x / lum_denom with the per-pixel reciprocal (div_by: the IEEE quotient for normal
             // results; lum_denom >= 0.001 and |x| <= 2 x 65504 for finite RGBA16F texels, and a
-            // quotient below the normal range rounds exp() to 1 either way)
-            float w_lum = hk_exp(div_by(-fabsf(l0[ch] - sl), lum_denom[ch], lum_rcp[ch]));
+            // quotient below the normal range rounds exp() to 1 either way); hk_exp_weight: hk_exp's bits
+            // for every argument a weight can take (<= 0, NaN clamped to 0 below)
+            float w_lum = hk_exp_weight(div_by(-fabsf(l0[ch] - sl), lum_denom[ch], lum_rcp[ch]));
             float w = hk_clampf(w_geo * w_lum, 0.0f, 1.0f) * kw;
             sum_irr[ch] = sum_irr[ch] + irr * w;
             sum_w[ch] += w;

@@ -33,6 +33,12 @@
 
 typedef union { float f; uint32_t u; int32_t i; } hk_fbits;
 
+/* Horner step of the exp2 / log2 polynomials: one fused multiply-add (correctly rounded on the CPU's fmaf and the
+ * GPU's v_fma_f32 alike, so both sides keep the same bits).  WGSL leaves exp2 / log2 implementation-defined; the
+ * build fixes them here.  Round 5: fused instead of a rounded product and sum (city 4K a-trous level 0.339 -> 0.325
+ * ms, profiles/r05/c6); the accuracy bound of test_transcendentals_accuracy (<= 4 ulp) still holds. */
+#define HK_MAD(a, b, c) fmaf((a), (b), (c))
+
 HK_HD uint32_t hk_f2u(float f) { hk_fbits b; b.f = f; return b.u; }
 HK_HD float hk_u2f(uint32_t u) { hk_fbits b; b.u = u; return b.f; }
 
@@ -56,13 +62,13 @@ HK_HD float hk_exp2(float x)
     float n = rintf(x);
     float f = x - n;
     float p = 1.5252733804059840e-05f;        /* ln2^7/7! */
-    p = p * f + 1.5403530393381608e-04f;      /* ln2^6/6! */
-    p = p * f + 1.3333558146428443e-03f;      /* ln2^5/5! */
-    p = p * f + 9.6181291076284772e-03f;      /* ln2^4/4! */
-    p = p * f + 5.5504108664821580e-02f;      /* ln2^3/3! */
-    p = p * f + 2.4022650695910071e-01f;      /* ln2^2/2! */
-    p = p * f + 6.9314718055994531e-01f;      /* ln2 */
-    p = p * f + 1.0f;
+    p = HK_MAD(p, f, 1.5403530393381608e-04f);      /* ln2^6/6! */
+    p = HK_MAD(p, f, 1.3333558146428443e-03f);      /* ln2^5/5! */
+    p = HK_MAD(p, f, 9.6181291076284772e-03f);      /* ln2^4/4! */
+    p = HK_MAD(p, f, 5.5504108664821580e-02f);      /* ln2^3/3! */
+    p = HK_MAD(p, f, 2.4022650695910071e-01f);      /* ln2^2/2! */
+    p = HK_MAD(p, f, 6.9314718055994531e-01f);      /* ln2 */
+    p = HK_MAD(p, f, 1.0f);
     /* n clamped before the conversion (only the selected cases use it: -151 <= n <= 128) */
     const int32_t ni = (int32_t)hk_minf(hk_maxf(n, -160.0f), 160.0f);
     const int normal = ni >= -126;
@@ -75,6 +81,31 @@ HK_HD float hk_exp2(float x)
 }
 
 HK_HD float hk_exp(float x) { return hk_exp2(x * 1.4426950408889634f); }
+
+/* hk_exp(x) without the selects of NaN and of x * log2(e) >= 128: the same bits for every x with x * log2(e) < 128
+ * and a NaN (of another payload, possibly) for NaN.  For the denoiser's edge-stopping weights (denoise.wgsl:44-69:
+ * exp of -|a| / b, b > 0), which are then clamped to [0, 1], where a NaN weight becomes 0 whatever its payload.
+ * Checked against hk_exp on every input (hko_exp_weight_mismatches). */
+HK_HD float hk_exp_weight(float x)
+{
+    const float y = x * 1.4426950408889634f;
+    float n = rintf(y);
+    float f = y - n;
+    float p = 1.5252733804059840e-05f;
+    p = HK_MAD(p, f, 1.5403530393381608e-04f);
+    p = HK_MAD(p, f, 1.3333558146428443e-03f);
+    p = HK_MAD(p, f, 9.6181291076284772e-03f);
+    p = HK_MAD(p, f, 5.5504108664821580e-02f);
+    p = HK_MAD(p, f, 2.4022650695910071e-01f);
+    p = HK_MAD(p, f, 6.9314718055994531e-01f);
+    p = HK_MAD(p, f, 1.0f);
+    const int32_t ni = (int32_t)hk_minf(hk_maxf(n, -160.0f), 160.0f);
+    const int normal = ni >= -126;
+    const float s1 = hk_u2f((uint32_t)(normal ? ni + 127 : ni + 64 + 127) << 23);
+    const float s2 = normal ? 1.0f : hk_u2f((uint32_t)(-64 + 127) << 23);
+    const float r = (p * s1) * s2;
+    return y < -151.0f ? 0.0f : r;
+}
 
 /* log2(x): x = m * 2^e with m in [sqrt(1/2), sqrt(2)); log2(m) via atanh series of s=(m-1)/(m+1).
  * Branch-free like hk_exp2 (x NaN -> x; x < 0 -> NaN; x == 0 -> -inf; x == +inf -> +inf; subnormal
@@ -92,10 +123,10 @@ HK_HD float hk_log2(float x)
     float s = (m - 1.0f) / (m + 1.0f);
     float s2 = s * s;
     float p = 0.11111111111111111f;          /* 1/9 */
-    p = p * s2 + 0.14285714285714285f;       /* 1/7 */
-    p = p * s2 + 0.2f;                       /* 1/5 */
-    p = p * s2 + 0.33333333333333333f;       /* 1/3 */
-    p = p * s2 + 1.0f;
+    p = HK_MAD(p, s2, 0.14285714285714285f);       /* 1/7 */
+    p = HK_MAD(p, s2, 0.2f);                       /* 1/5 */
+    p = HK_MAD(p, s2, 0.33333333333333333f);       /* 1/3 */
+    p = HK_MAD(p, s2, 1.0f);
     float lm = (p * s) * 2.8853900817779268f; /* 2/ln2 */
     float r = (float)e + lm;
     r = x == hk_u2f(0x7F800000u) ? x : r;

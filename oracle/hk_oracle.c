@@ -2533,7 +2533,8 @@ uint32_t hko_unpack_fast_mismatches(void)
     }
     return bad;
 }
-/* The branchy forms hk_math.h's hk_exp2 / hk_log2 had through round 4 (branch-free since round 5): the
+/* The branchy forms hk_math.h's hk_exp2 / hk_log2 had through round 4 (branch-free since round 5; the Horner steps
+ * are HK_MAD in both forms): the
  * count of inputs, over every stride-th of the 2^32 bit patterns (stride 1: all of them, ~50 s on 8
  * cores; 0 and 0 when last run), where the current form's bits differ from these (NaN payloads included) */
 static float exp2_branchy(float x)
@@ -2544,13 +2545,13 @@ static float exp2_branchy(float x)
     float n = rintf(x);
     float f = x - n;
     float p = 1.5252733804059840e-05f;
-    p = p * f + 1.5403530393381608e-04f;
-    p = p * f + 1.3333558146428443e-03f;
-    p = p * f + 9.6181291076284772e-03f;
-    p = p * f + 5.5504108664821580e-02f;
-    p = p * f + 2.4022650695910071e-01f;
-    p = p * f + 6.9314718055994531e-01f;
-    p = p * f + 1.0f;
+    p = HK_MAD(p, f, 1.5403530393381608e-04f);
+    p = HK_MAD(p, f, 1.3333558146428443e-03f);
+    p = HK_MAD(p, f, 9.6181291076284772e-03f);
+    p = HK_MAD(p, f, 5.5504108664821580e-02f);
+    p = HK_MAD(p, f, 2.4022650695910071e-01f);
+    p = HK_MAD(p, f, 6.9314718055994531e-01f);
+    p = HK_MAD(p, f, 1.0f);
     int32_t ni = (int32_t)n;
     if (ni >= -126) return p * hk_u2f((uint32_t)(ni + 127) << 23);
     return (p * hk_u2f((uint32_t)(ni + 64 + 127) << 23)) * hk_u2f((uint32_t)(-64 + 127) << 23);
@@ -2570,12 +2571,26 @@ static float log2_branchy(float x)
     float s = (m - 1.0f) / (m + 1.0f);
     float s2 = s * s;
     float p = 0.11111111111111111f;
-    p = p * s2 + 0.14285714285714285f;
-    p = p * s2 + 0.2f;
-    p = p * s2 + 0.33333333333333333f;
-    p = p * s2 + 1.0f;
+    p = HK_MAD(p, s2, 0.14285714285714285f);
+    p = HK_MAD(p, s2, 0.2f);
+    p = HK_MAD(p, s2, 0.33333333333333333f);
+    p = HK_MAD(p, s2, 1.0f);
     float lm = (p * s) * 2.8853900817779268f;
     return (float)e + lm;
+}
+/* hk_exp_weight against hk_exp over every stride-th input with x * log2(e) < 128 (NaN: both NaN) */
+unsigned long long hko_exp_weight_mismatches(uint32_t stride)
+{
+    unsigned long long bad = 0;
+    const long long n = ((1ll << 32) + stride - 1) / stride;
+#pragma omp parallel for schedule(static) reduction(+ : bad)
+    for (long long k = 0; k < n; ++k) {
+        const float x = hk_u2f((uint32_t)(k * (long long)stride));
+        if (!(x * 1.4426950408889634f < 128.0f) && x == x) continue;
+        const float a = hk_exp_weight(x), b = hk_exp(x);
+        if (x != x ? a == a : hk_f2u(a) != hk_f2u(b)) ++bad;
+    }
+    return bad;
 }
 void hko_math_form_mismatches(uint32_t stride, unsigned long long* out)
 {

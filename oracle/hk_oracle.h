@@ -80,6 +80,7 @@ float hko_exp2(float x);
 /* [exp2, log2]: inputs (every stride-th of the 2^32) where hk_math.h's branch-free forms differ from the round-4
  * branchy ones */
 void hko_math_form_mismatches(uint32_t stride, unsigned long long* out);
+unsigned long long hko_exp_weight_mismatches(uint32_t stride);
 float hko_log2(float x);
 float hko_sin(float x);
 float hko_cos(float x);

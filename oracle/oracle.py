@@ -56,6 +56,7 @@ def lib() -> C.CDLL:
         "hko_pow_int": (f, [f, C.c_int]),
         "hko_exp2": (f, [f]),
         "hko_math_form_mismatches": (None, [u32, vp]),
+        "hko_exp_weight_mismatches": (C.c_uint64, [u32]),
         "hko_log2": (f, [f]),
         "hko_sin": (f, [f]),
         "hko_cos": (f, [f]),

@@ -228,6 +228,12 @@ def test_branch_free_exp2_log2_equal_the_branchy_forms(oracle_lib):
     assert oracle_lib.hko_log2(float("inf")) == float("inf") and oracle_lib.hko_log2(2.0 ** -140) == -140.0
 
 
+def test_exp_weight_equals_exp(oracle_lib):
+    """hk_exp_weight (the denoise levels' weights) gives hk_exp's bits wherever x * log2(e) < 128, NaN for NaN:
+    every 5th input here (all of them: 0 when run with stride 1)."""
+    assert oracle_lib.hko_exp_weight_mismatches(5) == 0
+
+
 def test_pow_special_cases(oracle_lib):
     assert oracle_lib.hko_pow(0.0, 5.0) == 0.0
     assert oracle_lib.hko_pow(0.0, 0.25) == 0.0

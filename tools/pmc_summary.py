@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc passes written by tools/pmc.sh.
 
 usage: python tools/pmc_summary.py <pmc root dir> <config name> [--json profiles/pmc_traffic.json]
-                                   [--skip N] [--deep-json out.json "note"]
+                                   [--skip N] [--deep-json out.json "note"] [--levels]
 
 --skip N drops each kernel's first N dispatches of every profiled run (the warm-up frames: before the
 background-store-elision masks settle, frames 0-1 store every background pixel), so the averages are
@@ -17,6 +17,7 @@ hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.  (Exact for 16-B-per-lane
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -37,7 +38,14 @@ SHORT = {  # mangled and demangled spellings
 }
 
 
+LEVELS = "--levels" in sys.argv  # the a-trous levels per level (denoise_L0..L3) instead of one "denoise" row
+
+
 def short(name: str) -> str:
+    if LEVELS and "k_denoise3" in name:
+        m = re.search(r"k_denoise3(?:<\d+, (\d)>|ILi\dELi(\d)E)", name)
+        if m:
+            return f"denoise_L{m.group(1) or m.group(2)}"
     for k, v in SHORT.items():
         if k in name:
             return v
