@@ -419,6 +419,14 @@ HKD f2 load_depth_gradient(const Frame& F, const GBuffer& G, int32_t x, int32_t 
 }
 // integrator-plane (s) index of an in-frame pixel
 HKD int32_t s_index(const Frame& F, int32_t x, int32_t y) { return band_index(F, x, y, F.s[0], F.s_row0, F.s_rows); }
+// s_index of the passes that read neighbours (spatial reuse, the denoiser), which never run on interleaved stripes
+// (hk_render_frame / hk_denoise reject them): the row-band map alone
+HKD int32_t rb_index(const Frame& F, int32_t x, int32_t y)
+{
+    int32_t ly = y - F.s_row0;
+    ly = ly < 0 ? 0 : (ly >= F.s_rows ? F.s_rows - 1 : ly);
+    return x + (int32_t)F.s[0] * ly;
+}
 
 HKD f2 coords_to_uv(int32_t x, int32_t y, const uint32_t* size)
 {

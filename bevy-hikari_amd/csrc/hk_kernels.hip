@@ -1602,12 +1602,13 @@ struct DepthWin {
     const float* lds;  // null: no window (upscale ratio != 1)
     int32_t x0, y0;
 };
+// WINDOW: every coordinate the pass reads lies in the window — a neighbour is at most RANGE (20) px from its pixel
+// (f2i32 truncates toward zero, never outward) and a march tap between the two, so it is within 20 + 1 px of the
+// 16x16 tile and SP_HALO = 22 leaves a pixel to spare on each side — so the window is read without a bounds test
+template <bool WINDOW>
 HKD float win_depth(const Frame& F, const GBuffer& G, const DepthWin& W, int32_t x, int32_t y)
 {
-    if (W.lds) {
-        uint32_t lx = (uint32_t)(x - W.x0), ly = (uint32_t)(y - W.y0);
-        if (lx < (uint32_t)SP_WIN && ly < (uint32_t)SP_WIN) return W.lds[ly * SP_WIN + lx];
-    }
+    if constexpr (WINDOW) return W.lds[(y - W.y0) * SP_WIN + (x - W.x0)];
     return load_depth(F, G, x, y);
 }
 
@@ -1624,7 +1625,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
 {
     const Frame& F = A.F;
     constexpr uint32_t COUNT = EMISSIVE_LIT ? 8u : 16u;
-    const int32_t idx = s_index(F, x, y);
+    const int32_t idx = rb_index(F, x, y);
     const f2 uv = coords_to_uv(x, y, F.s);
     int32_t dx, dy;
     jittered_coords(F, uv, dx, dy);
@@ -1657,7 +1658,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     const bool from_previous = own.lifetime <= lifetime_max;
     int32_t previous_index = -1;  // load_previous's record; -1: outside the frame (the zero reservoir)
     if (from_previous && uv_inside_open(previous_uv))
-        previous_index = s_index(F, f2i32(previous_uv.x * (float)F.s[0]), f2i32(previous_uv.y * (float)F.s[1]));
+        previous_index = rb_index(F, f2i32(previous_uv.x * (float)F.s[0]), f2i32(previous_uv.y * (float)F.s[1]));
     float r_count = own.count, r_lifetime = own.lifetime, r_w_sum = own.w_sum, r_w2_sum = own.w2_sum;
     int32_t sel = SEL_OWN;
     if (from_previous) {
@@ -1713,7 +1714,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             if (suv.x < 0.0f || suv.y < 0.0f || suv.x > 1.0f || suv.y > 1.0f) continue;
             jittered_coords(F, suv, sdx, sdy);
         }
-        float sample_depth = win_depth(F, A.G, W, sdx, sdy);
+        float sample_depth = win_depth<WINDOW>(F, A.G, W, sdx, sdy);
         float depth_ratio = depth / sample_depth;
         if (depth_ratio < 0.9f || depth_ratio > 1.1f) continue;
         // the screen-space depth march first: it reads only the LDS depth window and rejects a third of
@@ -1739,7 +1740,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             } else {
                 jittered_coords(F, tuv, tdx, tdy);
             }
-            float tap_depth = win_depth(F, A.G, W, tdx, tdy);
+            float tap_depth = win_depth<WINDOW>(F, A.G, W, tdx, tdy);
             // j / (tap_count + 1) from the host table (tap_count <= 5 for RANGE <= 20)
             const float t = tap_count < 7u && j < 6u ? F.sp_tap_t[tap_count][j] : (float)j / (float)(tap_count + 1u);
             float ref_depth = hk_mixf(depth, sample_depth, t);
@@ -1752,7 +1753,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         // the neighbour's reservoir, its 16-byte planes loaded as the tests need them (the rejection
         // tests read plane 3 (count, normals) and plane 2 (sample position); planes 0-1 only for a
         // neighbour that is merged): the same values as load_res, fewer gathers for rejected ones
-        const int32_t nidx = s_index(F, scx, scy);
+        const int32_t nidx = rb_index(F, scx, scy);
         // the neighbour's record: the view planes (VIEW, store_res_view) or the reservoir's own 16-byte
         // planes, loaded as the tests need them (rejection: plane 3 count / normal, plane 2 sample
         // position; merge: planes 0-1): the same values as load_res either way
@@ -1951,14 +1952,7 @@ HKD bool bad3(f3 v)
     return __builtin_amdgcn_classf(v.x, NAN_PINF) || __builtin_amdgcn_classf(v.y, NAN_PINF) ||
            __builtin_amdgcn_classf(v.z, NAN_PINF);
 }
-// plane index of an integrator pixel for the denoiser, which never runs on interleaved stripes (hk_denoise
-// rejects them): s_index without the stripe map
-HKD int32_t dn_index(const Frame& F, int32_t x, int32_t y)
-{
-    int32_t ly = y - F.s_row0;
-    ly = ly < 0 ? 0 : (ly >= F.s_rows ? F.s_rows - 1 : ly);
-    return x + (int32_t)F.s[0] * ly;
-}
+
 // albedo plane is S-sized (band-local rows)
 HKD f4 load_albedo(const Frame& F, const uint2* albedo, int32_t x, int32_t y)
 {
@@ -2051,7 +2045,7 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
 // from the tile grown by the level's step on every side ((16 + 2 step)^2 texels: 4x the tile at step 8, 1.27x at
 // step 1); the workgroup copies that region once — each texel's (normal, depth), packed channels and instance,
 // three coalesced 16 / 16 / 8-byte loads — and the taps then read LDS instead of gathering ~37 scattered texels
-// per pixel through the caches.  Every value is the one a per-tap load would read (dn_index of the same
+// per pixel through the caches.  Every value is the one a per-tap load would read (rb_index of the same
 // coordinates) and the arithmetic per tap is the reference's, so the stored bits are those of the per-tap
 // version: city 4K 0.417 -> 0.354 ms per level (profiles/r05/c3).  Row stride: an odd multiple of 8 texels, so the
 // two 8-texel rows of a 16-lane LDS read phase fall in different halves of the banks.
@@ -2078,7 +2072,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         for (int32_t k = (int32_t)threadIdx.x; k < R::W * R::W; k += 256) {
             const int32_t ry = k / R::W, rx = k - ry * R::W;
             // out-of-frame texels are never tapped (the tap bounds test below); read at clamped coordinates
-            const int32_t sidx = dn_index(F, min(max(rx0 + rx, 0), (int32_t)F.s[0] - 1), min(max(ry0 + ry, 0), (int32_t)F.s[1] - 1));
+            const int32_t sidx = rb_index(F, min(max(rx0 + rx, 0), (int32_t)F.s[0] - 1), min(max(ry0 + ry, 0), (int32_t)F.s[1] - 1));
             const float4 nd = D.nd[sidx];
             const uint4 rgb = D.rgb[LEVEL][sidx];
             const uint2 bi = D.bi[LEVEL][sidx];
@@ -2091,7 +2085,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
     __syncthreads();
     int32_t x, y;
     if (!tile_pixel<DENOISE_ORDER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
-    const int32_t idx = dn_index(F, x, y);
+    const int32_t idx = rb_index(F, x, y);
     const int32_t oc = (y - y0 + step) * R::STRIDE + (x - x0 + step);  // the pixel in the region
     const float4 g0 = s_nd[oc];
     const uint2 cbi = s_bi[oc];

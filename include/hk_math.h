@@ -187,25 +187,26 @@ HK_HD float hk_cos_kernel(float r)
     return 1.0f + r2 * p;
 }
 
+/* Branch-free (round 5): both kernels computed, the quadrant's pair and the NaN / inf case selected — the same bits
+ * as the branchy form on every input (oracle hko_math_form_mismatches); 16 calls per spatial-reuse pixel. */
 HK_HD void hk_sincos(float x, float* s, float* c)
 {
-    if (x != x || hk_absf(x) == hk_u2f(0x7F800000u)) {
-        *s = hk_u2f(0x7FC00000u);
-        *c = *s;
-        return;
-    }
+    const int special = x != x || hk_absf(x) == hk_u2f(0x7F800000u);
     float k = rintf(x * 0.63661977236758134f); /* 2/pi */
     /* pi/2 split into three parts; the first two have short mantissas */
     float r = x - k * 1.5703125f;
     r = r - k * 4.837512969970703125e-4f;
     r = r - k * 7.54978995489188216e-8f;
-    int32_t q = ((int32_t)k) & 3;
-    float sk = hk_sin_kernel(r);
-    float ck = hk_cos_kernel(r);
-    if (q == 0) { *s = sk; *c = ck; }
-    else if (q == 1) { *s = ck; *c = -sk; }
-    else if (q == 2) { *s = -sk; *c = -ck; }
-    else { *s = -ck; *c = sk; }
+    /* k clamped before the conversion: |x| < 2^31 * pi/2 keeps it exact, larger |x| only select the quadrant */
+    const int32_t q = ((int32_t)hk_minf(hk_maxf(k, -2147483520.0f), 2147483520.0f)) & 3;
+    const float sk = hk_sin_kernel(r);
+    const float ck = hk_cos_kernel(r);
+    const int swap = q & 1;                  /* q = 1, 3: (s, c) = (+-ck, -+sk) */
+    const float a = swap ? ck : sk, b = swap ? sk : ck;
+    const float sa = (q == 2 || q == 3) ? -a : a;
+    const float sb = (q == 1 || q == 2) ? -b : b;
+    *s = special ? hk_u2f(0x7FC00000u) : sa;
+    *c = special ? hk_u2f(0x7FC00000u) : sb;
 }
 
 HK_HD float hk_sin(float x) { float s, c; hk_sincos(x, &s, &c); return s; }

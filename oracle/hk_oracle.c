@@ -2533,8 +2533,8 @@ uint32_t hko_unpack_fast_mismatches(void)
     }
     return bad;
 }
-/* The branchy forms hk_math.h's hk_exp2 / hk_log2 had through round 4 (branch-free since round 5; the Horner steps
- * are HK_MAD in both forms): the
+/* The branchy forms hk_math.h's hk_exp2 / hk_log2 / hk_sincos had through round 4 (branch-free since round 5; the
+ * Horner steps are HK_MAD in both forms): the
  * count of inputs, over every stride-th of the 2^32 bit patterns (stride 1: all of them, ~50 s on 8
  * cores; 0 and 0 when last run), where the current form's bits differ from these (NaN payloads included) */
 static float exp2_branchy(float x)
@@ -2592,18 +2592,45 @@ unsigned long long hko_exp_weight_mismatches(uint32_t stride)
     }
     return bad;
 }
+static void sincos_branchy(float x, float* s, float* c)
+{
+    if (x != x || hk_absf(x) == hk_u2f(0x7F800000u)) {
+        *s = hk_u2f(0x7FC00000u);
+        *c = *s;
+        return;
+    }
+    float k = rintf(x * 0.63661977236758134f);
+    float r = x - k * 1.5703125f;
+    r = r - k * 4.837512969970703125e-4f;
+    r = r - k * 7.54978995489188216e-8f;
+    int32_t q = ((int32_t)k) & 3;
+    float sk = hk_sin_kernel(r);
+    float ck = hk_cos_kernel(r);
+    if (q == 0) { *s = sk; *c = ck; }
+    else if (q == 1) { *s = ck; *c = -sk; }
+    else if (q == 2) { *s = -sk; *c = -ck; }
+    else { *s = -ck; *c = sk; }
+}
 void hko_math_form_mismatches(uint32_t stride, unsigned long long* out)
 {
-    unsigned long long be = 0, bl = 0;
+    unsigned long long be = 0, bl = 0, bs = 0;
     const long long n = ((1ll << 32) + stride - 1) / stride;
-#pragma omp parallel for schedule(static) reduction(+ : be, bl)
+#pragma omp parallel for schedule(static) reduction(+ : be, bl, bs)
     for (long long k = 0; k < n; ++k) {
         const float x = hk_u2f((uint32_t)(k * (long long)stride));
         if (hk_f2u(hk_exp2(x)) != hk_f2u(exp2_branchy(x))) ++be;
         if (hk_f2u(hk_log2(x)) != hk_f2u(log2_branchy(x))) ++bl;
+        /* sincos: inputs below 2^31 pi/2 in magnitude, where the branchy form's (int32_t)k is defined */
+        if (hk_absf(x) < 3.3e9f || x != x || hk_absf(x) == hk_u2f(0x7F800000u)) {
+            float s0, c0, s1, c1;
+            hk_sincos(x, &s0, &c0);
+            sincos_branchy(x, &s1, &c1);
+            if (hk_f2u(s0) != hk_f2u(s1) || hk_f2u(c0) != hk_f2u(c1)) ++bs;
+        }
     }
     out[0] = be;
     out[1] = bl;
+    out[2] = bs;
 }
 float hko_pow(float x, float y) { return hk_pow(x, y); }
 float hko_pow_int(float x, int n) { return n == 2 ? hk_pow2(x) : (n == 5 ? hk_pow5(x) : hk_pow16(x)); }

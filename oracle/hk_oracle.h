@@ -77,8 +77,8 @@ void hko_pack_reservoir_roundtrip(const float* fields, hk_packed_reservoir* pack
 float hko_pow(float x, float y);
 float hko_pow_int(float x, int n); /* n in {2, 5, 16} */
 float hko_exp2(float x);
-/* [exp2, log2]: inputs (every stride-th of the 2^32) where hk_math.h's branch-free forms differ from the round-4
- * branchy ones */
+/* [exp2, log2, sincos]: inputs (every stride-th of the 2^32) where hk_math.h's branch-free forms differ from the
+ * round-4 branchy ones */
 void hko_math_form_mismatches(uint32_t stride, unsigned long long* out);
 unsigned long long hko_exp_weight_mismatches(uint32_t stride);
 float hko_log2(float x);

@@ -214,13 +214,13 @@ def test_transcendentals_accuracy(oracle_lib, name, fn, lo, hi):
 
 
 def test_branch_free_exp2_log2_equal_the_branchy_forms(oracle_lib):
-    """hk_math.h's hk_exp2 / hk_log2 are written branch-free since round 5 (each case computed, the result
-    selected); they must give the bits of the round-4 branchy forms (kept in the oracle as the reference) on
-    every input.  Every 7th of the 2^32 bit patterns here (all of them: 0 / 0 when run with stride 1)."""
+    """hk_math.h's hk_exp2 / hk_log2 / hk_sincos are written branch-free since round 5 (each case computed, the
+    result selected); they must give the bits of the round-4 branchy forms (kept in the oracle as the reference) on
+    every input.  Every 7th of the 2^32 bit patterns here (all of them: 0 / 0 / 0 when run with stride 1)."""
     import ctypes as C
-    v = (C.c_uint64 * 2)()
+    v = (C.c_uint64 * 3)()
     oracle_lib.hko_math_form_mismatches(7, v)
-    assert list(v) == [0, 0], list(v)
+    assert list(v) == [0, 0, 0], list(v)
     # the selected special cases
     assert math.isnan(oracle_lib.hko_exp2(float("nan"))) and math.isnan(oracle_lib.hko_log2(-1.0))
     assert oracle_lib.hko_exp2(128.0) == float("inf") and oracle_lib.hko_exp2(-151.5) == 0.0
