@@ -39,7 +39,8 @@ import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Taa, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, halo_rows, reassembly_copies,  # noqa: E402
+from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, halo_rows, peer_exchange, peer_gather,  # noqa: E402
+                              reassembly_copies,  # noqa: E402
                               rebalance, stripe_gather_rows, use_stripes)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -333,9 +334,19 @@ def main():
         band = H
         r.resize(W, H, 1.0)
     row0, rows, core0, core_rows = r.band_info()
-    # the gathered rows back in frame order (stripes; uneven bands) on a side stream after each gather
-    # (nothing to put back when the gathered rows are already in frame order: one rank, equal bands)
-    reorder = dist_on and not np.array_equal(gather_index, np.arange(H)) if (stripes or bounds is not None) else False
+    # How the ranks' rows reach every rank (HK_BENCH_GATHER): "peer" (the default) sends each rank's rows straight
+    # to every peer while receiving every peer's rows on that peer's own xGMI link (batch_isend_irecv: N-1
+    # transfers of one band each at once, instead of a ring moving (N-1)/N of the frame through one link).  Row
+    # bands are exchanged in place in a whole-frame buffer (bands.peer_exchange: each band lands in its rows, no
+    # reassembly); the interleaved stripes' padded rows go into the all-gather's layout (bands.peer_gather) and are
+    # put back in frame order as before.  "ring": one all-gather of the padded rows (RCCL's ring), reassembled on a
+    # side stream when not already in frame order (stripes, uneven bands).
+    gather_mode = os.environ.get("HK_BENCH_GATHER", "peer")
+    peer = dist_on and not stripes and gather_mode == "peer"
+    peer_stripes = dist_on and stripes and gather_mode == "peer"
+    my_y0 = band_of(rank, world, H, bounds).y0 if peer else 0
+    reorder = (dist_on and not peer and not np.array_equal(gather_index, np.arange(H))
+               if (stripes or bounds is not None) else False)
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
@@ -345,9 +356,10 @@ def main():
     comm = torch.cuda.Stream() if dist_on else None
     # double-buffered band / gathered frame: the all-gather of frame f runs on RCCL's stream
     # while frame f+1 renders; a buffer is reused only after its previous gather completed
-    band_t = [torch.zeros((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
+    band_t = [torch.zeros((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] if not peer else None
     full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
-        if dist_on else None
+        if dist_on and not peer else None
+    peer_t = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] if peer else None
     pending = [None, None]
     if reorder:  # stripes / uneven bands back in frame order, on a side stream after each gather
         frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
@@ -417,29 +429,54 @@ def main():
     # "noreorder" = copy + all-gather without the frame-order reorder, "none" = nothing
     comm_mode = os.environ.get("HK_BENCH_COMM", "full")
 
+    def wait_all(p):
+        for q in (p if isinstance(p, list) else [p]):
+            q.wait()
+
     def gather(f, plane):
         gathered[0] = f
         if comm_mode == "none":
             return
         k = f & 1
+        if peer:
+            with torch.cuda.stream(comm):
+                if pending[k] is not None:
+                    wait_all(pending[k])  # device-side: the comm stream waits for that exchange
+                r.copy_output_rows(plane, core0, core_rows, peer_t[k][my_y0].data_ptr(), False, comm.cuda_stream)
+                if comm_mode == "copy":
+                    return
+                if rehearsal:  # gloo on one GPU: the exchange through host copies
+                    host = peer_t[k].cpu()
+                    wait_all(peer_exchange(host, bounds, rank, world))
+                    peer_t[k].copy_(host)
+                else:
+                    pending[k] = peer_exchange(peer_t[k], bounds, rank, world)
+            return
         with torch.cuda.stream(comm):
             if pending[k] is not None:
-                pending[k].wait()  # device-side: the comm stream waits for that gather
+                wait_all(pending[k])  # device-side: the comm stream waits for that gather
             if reorder and reorder_done[k] is not None:
                 comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
             r.copy_output_rows(plane, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
             if comm_mode == "copy":
                 return
             if rehearsal:
-                parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
-                dist.all_gather(parts, band_t[k].cpu())
-                full_t[k].copy_(torch.cat(parts))
+                if peer_stripes:
+                    host = torch.empty((world * band, W, 4), dtype=torch.float16)
+                    wait_all(peer_gather(host, band_t[k].cpu(), rank, world))
+                    full_t[k].copy_(host)
+                else:
+                    parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
+                    dist.all_gather(parts, band_t[k].cpu())
+                    full_t[k].copy_(torch.cat(parts))
+            elif peer_stripes:
+                pending[k] = peer_gather(full_t[k], band_t[k], rank, world)
             else:
                 pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
         if reorder and comm_mode != "noreorder":
             with torch.cuda.stream(side):
                 if pending[k] is not None:
-                    pending[k].wait()
+                    wait_all(pending[k])
                 else:
                     side.wait_stream(comm)
                 if row_copies is not None:
@@ -454,7 +491,7 @@ def main():
             gather(last, shown)
         for k in range(2):
             if pending[k] is not None:
-                pending[k].wait()
+                wait_all(pending[k])
                 pending[k] = None
         torch.cuda.current_stream().wait_stream(comm)
         if reorder:
@@ -582,9 +619,12 @@ def main():
                        "options": {k: v for k, v in r.options().items()},
                        "rays_per_frame": int(rays // (args.steps * spp)),
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
-                       "parallelism": (f"interleaved 8-row stripes x{world} + RCCL all-gather" if stripes else
-                                       f"cost-balanced row-bands x{world} + RCCL all-gather") if world > 1 else
-                                      ("single GPU through the RCCL path (world size 1)" if dist_on else "single GPU"),
+                       "parallelism": (f"interleaved 8-row stripes x{world}" if stripes else
+                                       f"cost-balanced row-bands x{world}") +
+                                      (" + RCCL per-peer exchange" if gather_mode == "peer" else " + RCCL all-gather")
+                                      if world > 1 else
+                                      (f"single GPU through the RCCL path (world size 1, {gather_mode} gather)"
+                                       if dist_on else "single GPU"),
                        "band_bounds": None if bounds is None else [int(v) for v in bounds],
                        "band_calibration": balance or None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

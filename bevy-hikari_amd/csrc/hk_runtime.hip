@@ -189,6 +189,8 @@ struct hk_ctx {
     // indirect channel; valid = the mask describes the buffers' contents for pass window key
     uint8_t* bgmask[2] = {};
     bool bg_valid[2] = {false, false};
+    // a band's per-channel row-window margins, sticky maxima since hk_resize (band_windows): -1 = none yet
+    int32_t win_out = -1, win_emi = -1, win_ind = -1;
     int32_t bg_key[2][2] = {};
     uint8_t* gbmask = nullptr;  // the G-buffer's (ViewArgs::bg), per S pixel
     uint4* sp_view = nullptr;   // spatial view planes of the indirect channel (ChannelArgs::view), 3 x res_n
@@ -661,8 +663,8 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
 // For a static camera every other read is the pixel's own (temporal reprojection is the
 // identity), so the core rows stay bit-identical to the whole frame (test_gpu_row_bands_*),
 // with 1.15x instead of 1.30x the work of an 8-way city 4K band.  Rows outside a pass's window
-// keep stale values that no windowed pass reads (a settings change that widens a window later reads
-// them: band outputs are exact for a fixed setting).  Option band_full_windows: every pass on all rows.
+// keep stale values that no windowed pass reads; a settings change that widens a window (band_windows) zeroes
+// the rows it brings in and keeps the window wide from then on.  Option band_full_windows: every pass on all rows.
 constexpr int32_t DENOISE_OUT_REACH = 16, SPATIAL_RANGE = 20, EMISSIVE_SPATIAL_RANGE = 10;
 constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
 // Only for a static frame: under camera or instance motion temporal reprojection reads the previous
@@ -682,10 +684,45 @@ FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
 // masks are both dropped while it is off)
 bool bg_elision_off(const hk_ctx* c) { return !c->on(OPT_BG_ELISION); }
 int32_t light_out_reach(const hk_settings* st) { return st->denoise ? DENOISE_OUT_REACH : 0; }
-int32_t spatial_range(const hk_settings* st)
+// The settings-dependent margins of a band's light-pass windows (pass_window) as sticky maxima: a
+// setting turned on later (denoise, emissive or indirect spatial reuse) widens its channel's window, and the rows
+// it brings in hold reservoirs no pass has updated since the band was sized (or since a motion frame ran every
+// pass on the whole band).  Those rows' records of the channel's buffers are zeroed when the window first grows,
+// as hk_resize zero-fills them (light.rs:355-358), and the window then never narrows again, so every later toggle
+// of the setting is exact again.  The frame that widens the window differs from a whole-frame render near the
+// band's core edges (its new rows start without history): test_gpu_row_bands_settings_toggle.
+int band_windows(hk_ctx* c, const FrameArgs& A_all, const hk_settings* st, hipStream_t s)
 {
-    return st->indirect_spatial_reuse ? SPATIAL_RANGE : (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0);
+    const int32_t out = light_out_reach(st);
+    const int32_t want[3] = {out, out + (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0),
+                             out + (st->indirect_spatial_reuse ? SPATIAL_RANGE : 0)};
+    int32_t* have[3] = {&c->win_out, &c->win_emi, &c->win_ind};
+    // the buffers whose records the group's window holds: spatial pairs 4/5, 8/9; direct + emissive 0-5; indirect 6-9
+    static const int first[3][2] = {{4, 8}, {0, -1}, {6, -1}};
+    static const int count[3][2] = {{2, 2}, {6, 0}, {4, 0}};
+    const bool windowed = pass_window(c, A_all, 0).F.win_rows > 0;
+    for (int g = 0; g < 3; ++g) {
+        const int32_t old = *have[g], m = std::max(old, want[g]);
+        if (m == old) continue;
+        *have[g] = m;
+        if (old < 0 || !windowed) continue;  // zero-filled since hk_resize, or every row computed this frame
+        const int32_t w = (int32_t)c->s[0], core0 = c->core_row0, core1 = c->core_row0 + c->core_rows;
+        const int32_t span[2][2] = {{std::max(0, core0 - m), std::max(0, core0 - old)},
+                                    {std::min(c->s_rows, core1 + old), std::min(c->s_rows, core1 + m)}};
+        for (int k = 0; k < 2; ++k)
+            for (int b = 0; b < count[g][k]; ++b)
+                for (int side = 0; side < 2; ++side) {
+                    const int32_t r0 = span[side][0], r1 = span[side][1];
+                    if (r1 <= r0) continue;
+                    for (uint32_t plane = 0; plane < 4; ++plane)
+                        HK_HIP(c, hipMemsetAsync(c->reservoirs[first[g][k] + b] + (size_t)plane * c->res_n + (size_t)r0 * w, 0,
+                                                 (size_t)(r1 - r0) * w * sizeof(uint4), s));
+                }
+        c->bg_valid[0] = c->bg_valid[1] = false;  // the elision masks no longer describe the buffers
+    }
+    return HK_OK;
 }
+
 
 // The primary rays a k_gbuffer launch over A counts (its active pixels on the rows it counts: k_gbuffer's
 // n_primary), for the launches G-buffer reuse skips.
@@ -841,6 +878,9 @@ int hk_set_option(hk_ctx* c, const char* key, double value)
         if (std::strcmp(OPTS[k].key, key) != 0) continue;
         if (!(value >= OPTS[k].lo && value <= OPTS[k].hi))
             return fail(c, HK_ERR_INVALID, std::string("option ") + key + " out of range");
+        // every key but the pixel-count thresholds is an on/off switch or a mode: integers only
+        if (!std::strstr(key, "_min_px") && value != std::floor(value))
+            return fail(c, HK_ERR_INVALID, std::string("option ") + key + " takes an integer value");
         c->opt[k] = value;
         c->gen++;  // (G-buffer reuse: planes written under other options are not reused)
         if (k == OPT_BAND_FULL_WINDOWS) c->bg_valid[0] = c->bg_valid[1] = c->gb_valid = false;  // new windows
@@ -1224,6 +1264,7 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
         HK_HIP(c, hipMemset(c->denoised[i], 0, sp * sizeof(uint2)));
     }
     c->res_n = (uint32_t)sp;
+    c->win_out = c->win_emi = c->win_ind = -1;
     for (int i = 0; i < HK_RESERVOIR_BUFFERS; ++i) {
         HK_HIP(c, hipMalloc(&c->reservoirs[i], 4 * sp * sizeof(uint4)));
         HK_HIP(c, hipMemset(c->reservoirs[i], 0, 4 * sp * sizeof(uint4)));  // light.rs:355-358 zero-fill
@@ -1619,9 +1660,11 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // per-pass row windows of a band (pass_window): each channel's temporal pass on the rows its spatial
     // pass reads (core +-(OUT + that channel's range): direct_lit has no spatial pass, light.rs:656-676),
     // then spatial reuse.  A: the indirect channel; AE: direct + emissive.
-    A = pass_window(c, A_all, light_out_reach(settings) + (settings->indirect_spatial_reuse ? SPATIAL_RANGE : 0));
-    FrameArgs AE = pass_window(c, A_all, light_out_reach(settings) + (settings->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0));
-    const FrameArgs AS = pass_window(c, A_all, light_out_reach(settings));
+    // (sticky margins: band_windows)
+    HK_TRY(band_windows(c, A_all, settings, st));
+    A = pass_window(c, A_all, c->win_ind);
+    FrameArgs AE = pass_window(c, A_all, c->win_emi);
+    const FrameArgs AS = pass_window(c, A_all, c->win_out);
     ChannelArgs C0 = channel(c, A.F.number, 0);
     ChannelArgs C1 = channel(c, A.F.number, 1);
     // direct_lit + emissive in one launch when every reprojection is the identity: see
@@ -1669,7 +1712,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     const bool merge_default = !pipeline_size(c) && !settings->indirect_spatial_reuse && !settings->emissive_spatial_reuse;
     const bool merge = merge_possible && (c->opt[OPT_MERGE] < 0.0 ? merge_default : c->on(OPT_MERGE));
     // (one grid for all three channels: the wider window)
-    if (merge) A = AE = pass_window(c, A_all, light_out_reach(settings) + spatial_range(settings));
+    if (merge) A = AE = pass_window(c, A_all, std::max(c->win_ind, c->win_emi));
     if (fork && !merge) {
         if (gb_fresh && c->rf_side_only && swap && c->albedo_fresh && !had_ext) {
             // The fork marker would make the side stream wait for the caller stream here.  What the
@@ -1751,7 +1794,10 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     hipStream_t st = async ? c->dn_stream : caller;
     if (async) HK_TRY(tail_begin(c));
     else HK_TRY(gb_join(c, st));
-    for (int ch = 0; ch < 3; ++ch) HK_TRY(ext_wait(c, st, c->denoised[ch]));
+    for (int ch = 0; ch < 3; ++ch) {
+        HK_TRY(ext_wait(c, st, c->denoised[ch]));
+        HK_TRY(ext_wait(c, st, c->internal_variance[ch]));  // HK_OUT_DENOISE_INTERNAL_VARIANCE copies
+    }
     FrameArgs A = frame_args(c, settings, in);
     int channels = settings->indirect_bounces == 0u ? 2 : 3;  // post_process.rs:949-954
     DenoiseArgs D;
@@ -2044,6 +2090,17 @@ int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* d
                              to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
     if (to_host) HK_HIP(c, hipStreamSynchronize(st));
     if (foreign) {
+        // entries whose copies have completed go back to the pool (a plane nobody rewrites would otherwise keep its
+        // entries, and ext_reads would grow with every copy of it)
+        for (size_t k = 0; k < c->ext_reads.size();) {
+            if (hipEventQuery(c->ext_reads[k].second) == hipSuccess) {
+                c->ext_pool.push_back(c->ext_reads[k].second);
+                c->ext_reads[k] = c->ext_reads.back();
+                c->ext_reads.pop_back();
+            } else {
+                ++k;
+            }
+        }
         hipEvent_t e = nullptr;
         if (!c->ext_pool.empty()) {
             e = c->ext_pool.back();

@@ -142,3 +142,49 @@ def reassembly_copies(frame, gathered, world: int, height: int, pad: int, bounds
             dst, src = frame[b.y0: b.y0 + b.rows], gathered[q * pad: q * pad + b.rows]
         out.append((dst, src))
     return out
+
+
+# ---------------------------------------------------------------- per-peer gather (row bands)
+# A ring all-gather moves (N-1)/N of the frame through each GPU's busiest xGMI link, one band per step; an MI355X
+# node connects every GPU to every other one (7 links of ~153 GB/s per GPU), so each rank can instead send its band
+# straight to every peer and receive every peer's band on that peer's own link: N-1 transfers at once, each the size
+# of one band (cornell 1080p at N = 8: 0.518 MB per link instead of 3.6 MB through one).
+# The bands are contiguous rows, so each peer's band lands directly in its place in the frame: no reassembly pass
+# for uneven (cost-balanced) bands either.
+def peer_exchange_ops(frame, bounds, rank: int, world: int) -> list:
+    """The point-to-point operations of the per-peer gather over `frame` (rows x ... tensor holding the whole frame,
+    this rank's rows [bounds[rank], bounds[rank + 1]) already in place): this rank's rows sent to every peer, every
+    peer's rows received into their place.  For torch.distributed.batch_isend_irecv (RCCL runs the group's
+    transfers together).  Peers are visited in a staggered order (rank + k, rank - k) so that no rank is every
+    rank's first partner."""
+    import torch.distributed as dist
+    mine = frame[bounds[rank]: bounds[rank + 1]]
+    ops = []
+    for k in range(1, world):
+        dst, src = (rank + k) % world, (rank - k) % world
+        ops.append(dist.P2POp(dist.isend, mine, dst))
+        ops.append(dist.P2POp(dist.irecv, frame[bounds[src]: bounds[src + 1]], src))
+    return ops
+
+
+def peer_exchange(frame, bounds, rank: int, world: int) -> list:
+    """Start the per-peer gather; returns the requests (wait() each)."""
+    import torch.distributed as dist
+    ops = peer_exchange_ops(frame, bounds, rank, world)
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
+def peer_gather(full, mine, rank: int, world: int) -> list:
+    """The per-peer form of all_gather_into_tensor(full, mine) for the interleaved stripes' padded rows (or any
+    equal-size parts): `mine` sent to every peer, peer j's part received into full[j * n : (j + 1) * n] (n =
+    len(mine)), this rank's own part copied into its slot; returns the requests (wait() each).  The slots keep the
+    all-gather's layout, so bench.py's reassembly (reassembly_copies / stripe_gather_rows) applies unchanged."""
+    import torch.distributed as dist
+    n = mine.shape[0]
+    full[rank * n: (rank + 1) * n].copy_(mine)
+    ops = []
+    for k in range(1, world):
+        dst, src = (rank + k) % world, (rank - k) % world
+        ops.append(dist.P2POp(dist.isend, mine, dst))
+        ops.append(dist.P2POp(dist.irecv, full[src * n: (src + 1) * n], src))
+    return dist.batch_isend_irecv(ops) if ops else []

@@ -221,7 +221,8 @@ void hk_settings_default(hk_settings* out);
  *                            compacted batch (long walks first) on frames without emissive validation
  *   compact_shadow (0)       shadow walks of a workgroup as one compacted batch (fused launch, indirect pass)
  *                            (both measured slower than the per-pixel walks: DESIGN §4)
- * hk_set_option returns HK_ERR_INVALID for an unknown key or a value outside the key's range. */
+ * hk_set_option returns HK_ERR_INVALID for an unknown key, a value outside the key's range, or a fractional value
+ * for any key but the *_min_px thresholds. */
 int hk_set_option(hk_ctx* ctx, const char* key, double value);
 int hk_get_option(const hk_ctx* ctx, const char* key, double* value);
 /* key of option `index` (0, 1, ...; NULL past the last one) */

@@ -309,6 +309,61 @@ def test_gpu_row_bands_match_whole_frame(spatial, denoise, world, H):
     assert total == o.counters()
 
 
+def test_gpu_row_bands_settings_toggle():
+    """A band's light-pass windows depend on the settings (hk_runtime.hip pass_window: each channel's temporal pass on
+    core +-(OUT + its spatial range)); turning emissive spatial reuse on at frame 4 widens the direct / emissive
+    window, and the rows it brings in have no reservoir history.  band_windows zeroes them and keeps the window
+    wide from then on.  Before the toggle every band's core rows equal the whole-frame render bit for
+    bit.  While emissive spatial reuse is on, it reads the new rows' emissive records, whose history started at the
+    toggle, so the core rows near the bands' edges differ: measured 93-98 % of pixels exact, mean relative difference
+    <= 1.5e-4 (profiles/r05/c9), held here to >= 90 % and <= 2e-3.  With the setting off again (frame 7) nothing reads
+    those rows and the core rows are bit-exact again; turning it on once more (frames 8-9) changes no window."""
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
+    from hikari_amd.bands import band_of, halo_rows
+    from oracle import Oracle
+    W, H, world = 64, 192, 3
+    scene, cam, lights = examples.cornell()
+    desc = scene.build()
+    on = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, emissive_spatial_reuse=True,
+                        denoise=True).to_c()
+    off = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, emissive_spatial_reuse=False,
+                         denoise=True).to_c()
+    o = Oracle(desc, load_noise(), W, H, 1.0)
+    ranks = []
+    for k in range(world):
+        b = band_of(k, world, H)
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.set_band_halo(halo_rows(True, True))
+        r.resize(W, H, 1.0, b.y0, b.rows)
+        ranks.append((b, r))
+    errors, worst = [], []
+    for f in range(10):
+        s = on if 4 <= f < 7 or f >= 8 else off
+        fi = frame_inputs(f, cam, lights, W, H)
+        for x in [o] + [r for _, r in ranks]:
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        whole = canon_plane(10, o.output(10)).reshape(H, W, 4)
+        for b, r in ranks:
+            row0, rows, core0, core_rows = r.band_info()
+            a = canon_plane(10, r.output(10)[core0: core0 + core_rows]).reshape(core_rows, W, 4)
+            c = whole[b.y0: b.y0 + b.rows]
+            exact = float((a == c).all(axis=-1).mean())
+            fa = a.view(np.float16).astype(np.float32)[..., :3]
+            fc = c.view(np.float16).astype(np.float32)[..., :3]
+            rel = float(np.abs(fa - fc).sum() / max(np.abs(fc).sum(), 1e-6))
+            worst.append((f, b.y0, round(exact, 4), round(rel, 5)))
+            if (f < 4 or f == 7) and exact < 1.0:
+                errors.append(f"frame {f} band {b.y0}: {exact:.4f} of pixels exact with emissive spatial reuse off")
+            if exact < 0.90 or rel > 0.002:
+                errors.append(f"frame {f} band {b.y0}: {exact:.4f} of pixels exact, mean relative difference {rel:.4f}")
+    assert not errors, "\n".join(errors) + f"\n{worst}"
+
+
 def test_gpu_row_bands_moving_camera_within_tolerance():
     """Band contexts under camera motion (the examples' orbit, examples.orbit at 2 deg/frame): every pass
     then runs on the whole band (pass_window keeps row windows for static frames only), and temporal

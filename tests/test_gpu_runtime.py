@@ -4,7 +4,8 @@ the same frames with the feature switched off through hk_set_option:
 * foreign-stream output copies (hk_copy_output_rows on a communication stream, as bench.py's all-gather
   path issues them): each copy sees its frame's finished plane while the frames stay pipelined, and the
   plane's next write waits for the copy;
-* a row band fed host G-buffer planes with motion runs every pass on its whole band.
+* a row band fed host G-buffer planes with motion runs every pass on its whole band (ADVICE r03);
+* foreign-stream copies of the denoiser's internal variance, and the option value checks.
 """
 import copy
 import ctypes
@@ -170,6 +171,60 @@ def test_foreign_stream_copies_keep_frames_exact(denoise):
     for b in bufs:
         hip.hipFree(b)
     hip.hipStreamDestroy(stream)
+
+
+def test_foreign_copies_of_the_internal_variance():
+    """hk_copy_output_rows of HK_OUT_DENOISE_INTERNAL_VARIANCE on a foreign stream registers a read of
+    that plane, so the next hk_denoise (which rewrites it) waits for the copy.  Each frame's copy must hold that
+    frame's plane (the oracle's), with frames queued pipelined behind the copies."""
+    from hikari_amd import HikariSettings, Upscale, _abi, frame_inputs
+    hip = _hip()
+    w, h = 96, 72
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=True)
+    scene, cam, lights, r, o = _pair("cornell", w, h, st, options={"pipeline_min_px": 0})
+    s = st.to_c()
+    stream = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(stream)) == 0
+    nbytes = h * w * 4
+    bufs = [ctypes.c_void_p() for _ in range(4)]
+    for b in bufs:
+        assert hip.hipMalloc(ctypes.byref(b), nbytes) == 0
+    want = []
+    for f in range(4):
+        fi = frame_inputs(f, cam, lights, w, h)
+        r.render_gbuffer(fi)
+        r.render_frame(s, fi)
+        r.denoise(s, fi)
+        r.tone_sum(s)
+        r.copy_output_rows(_abi.OUT_DENOISE_INTERNAL_VARIANCE, 0, h, bufs[f].value, False, stream.value)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.denoise(s, fi)
+        want.append(canon_plane(16, o.output(16)))
+    assert hip.hipStreamSynchronize(stream) == 0
+    for f in range(4):
+        out = np.empty((h, w, 4), np.uint8)
+        assert hip.hipMemcpy(out.ctypes.data, bufs[f], nbytes, 2) == 0
+        m = mismatch_report(canon_plane(16, out), want[f], f"frame {f} internal variance copy")
+        assert not m, m
+    for b in bufs:
+        hip.hipFree(b)
+    hip.hipStreamDestroy(stream)
+
+
+def test_option_values():
+    """hk_set_option: on/off switches and modes take integers only (0.5 used to count as on), the
+    pixel-count thresholds any value in range; unknown keys and out-of-range values are refused."""
+    from hikari_amd import HikariRenderer
+    from hikari_amd._abi import HikariError
+    r = HikariRenderer(0)
+    for key, bad in (("gbuffer_reuse", 0.5), ("lds_scene", 1.5), ("merge", 0.3), ("lds_scene", 3), ("nope", 1)):
+        with pytest.raises(HikariError):
+            r.set_option(key, bad)
+    r.set_option("fuse_min_px", 1234.5)
+    r.set_option("lds_scene", 2)
+    r.set_option("merge", -1)
+    assert (r.get_option("fuse_min_px"), r.get_option("lds_scene"), r.get_option("merge")) == (1234.5, 2.0, -1.0)
 
 
 def test_band_with_host_planes_under_motion_runs_whole_band():

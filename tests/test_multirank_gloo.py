@@ -226,6 +226,104 @@ def test_balanced_uneven_bands_reassemble_whole_frame(world):
     assert np.array_equal(gathered, whole)
 
 
+def _peer_worker(rank, world, port, balanced, q):
+    """bench.py's per-peer gather (HK_BENCH_GATHER=peer, bands.peer_exchange): each rank renders its band + halo,
+    places its own rows in a whole-frame buffer and exchanges bands point to point with every peer
+    (batch_isend_irecv); every rank must end with the whole frame."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    for p in (root / "bevy-hikari_amd", root / "oracle", root / "tests"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    from hikari_amd.bands import band_of, equal_bounds, halo_rows, peer_exchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bounds = equal_bounds(world, H)
+    if balanced:  # uneven bands on 8-row multiples
+        bounds = [0] + [int(round(H * (k / world) ** 1.5 / 8)) * 8 for k in range(1, world)] + [H]
+    band = band_of(rank, world, H, bounds)
+    img = _render(band, halo_rows(True, True))
+    frame = torch.full((H, W, 8), 0xAB, dtype=torch.uint8)
+    frame[band.y0: band.y0 + band.rows] = torch.from_numpy(np.ascontiguousarray(img[band.y0: band.y0 + band.rows]))
+    for req in peer_exchange(frame, bounds, rank, world):
+        req.wait()
+    q.put((rank, frame.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,balanced", [(2, False), (4, False), (3, True)])
+def test_peer_exchange_gathers_whole_frame(world, balanced):
+    """The per-peer gather (direct band transfers instead of the ring all-gather) leaves every rank with the
+    whole-frame render, for equal and uneven bands."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer_worker, args=(r, world, port, balanced, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    whole = _render(None, 0, True, True)
+    for rank in range(world):
+        assert np.array_equal(frames[rank], whole), rank
+
+
+def _stripe_peer_worker(rank, world, port, q):
+    """bench.py's interleaved stripes with the per-peer gather (bands.peer_gather into the all-gather's padded
+    layout, then stripe_gather_rows' reassembly)."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    for p in (root / "bevy-hikari_amd", root / "oracle", root / "tests"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    from hikari_amd.bands import peer_gather, stripe_gather_rows, stripe_rows
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    img = _render(None, 0, False, False, stripes=(rank, world))
+    pad, index = stripe_gather_rows(world, H)
+    rows = stripe_rows(rank, world, H)
+    mine = np.zeros((pad, W, 8), np.uint8)
+    mine[:len(rows)] = img[rows]
+    full = torch.empty((world * pad, W, 8), dtype=torch.uint8)
+    for req in peer_gather(full, torch.from_numpy(mine), rank, world):
+        req.wait()
+    q.put((rank, full.numpy()[index].copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_stripes_peer_gather_reassemble_whole_frame(world):
+    """The interleaved stripes gathered per peer (bench.py's default for frames without neighbour reads) and put
+    back in frame order equal the whole-frame render on every rank."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stripe_peer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    whole = _render(None, 0, False, False)
+    for rank in range(world):
+        assert np.array_equal(frames[rank], whole), rank
+
+
 def test_rebalance_converges_on_a_skewed_cost():
     """bands.rebalance on a known per-row cost (city-like: the lower rows 6x as costly), each band's
     time = its rows' cost + a fixed per-band cost: three rounds bring the slowest band within 6 % of the

@@ -6,17 +6,20 @@ the N-GPU frame (the RCCL all-gather of frame f overlaps frame f+1 in bench.py).
 the strong-scaling curve when no multi-GPU box is at hand; it is not a multi-GPU measurement.
 Frames without neighbour reads use bench.py's interleaved stripes (--bands: contiguous bands).
 
-The projection adds the collective: one all-gather of the tone-mapped RGBA16F frame
-(8 B/px) per displayed frame, whose ring moves (N-1)/N of the frame through each GPU's busiest xGMI
-link at ~153 GB/s (MI355X: 7 links x ~153 GB/s per GPU).  bench.py double-buffers it, so the gather of
-frame f runs on RCCL's stream next to frame f+1: frame time = max(compute, gather) when it overlaps,
-compute + gather when it does not; both are printed.
+The projection adds the collective: one gather of the tone-mapped RGBA16F frame (8 B/px) per
+displayed frame.  bench.py's default per-peer gather (HK_BENCH_GATHER=peer, bands.peer_exchange / peer_gather)
+sends each rank's rows straight to every peer over that pair's own xGMI link, so it is bound by one band per link
+at ~153 GB/s (MI355X: 7 links x ~153 GB/s per GPU); --gather ring models the all-gather ring instead, which moves
+(N-1)/N of the frame through each GPU's busiest link.  bench.py double-buffers it, so the gather of frame f runs
+next to frame f+1: frame time = max(compute, gather) when it overlaps, compute + gather when it does not; both
+are printed.
 Row bands are cost-balanced as bench.py balances them (bands.rebalance, --balance R rounds, default 5:
 every rank's band timed, the boundaries moved to equal measured cost, timed again); the equal-row split is
 printed beside it.  --overhead-ms X adds the measured per-frame cost of the collective path itself (the
 band copy, the all-gather's stream waits and the reorder at world size 1: HK_BENCH_DIST=1 minus the
 single-GPU line) to every N > 1 frame.
-usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N] [--balance R] [--overhead-ms X]"""
+usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N] [--balance R] [--overhead-ms X]
+                                   [--gather peer|ring]"""
 import json
 import sys
 import time
@@ -29,7 +32,7 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "bevy-hikari_amd"))
 import bench  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import band_of, equal_bounds, halo_rows, rebalance, use_stripes  # noqa: E402
+from hikari_amd.bands import band_of, equal_bounds, halo_rows, rebalance, stripe_gather_rows, use_stripes  # noqa: E402
 
 cfg_name = sys.argv[1] if len(sys.argv) > 1 else "cornell-1080p-nee"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 50
@@ -49,11 +52,18 @@ def allgather_ms(n: int) -> float:
     return 0.0 if n == 1 else (n - 1) / n * W * H * 8 / (XGMI_LINK_GBS * 1e9) * 1e3
 
 
+def peer_gather_ms(n: int, part_rows: int) -> float:
+    """Per-peer gather: every pair of GPUs exchanges one part (the largest band, or a rank's padded stripe rows) on
+    its own link, all links at once."""
+    return 0.0 if n == 1 else part_rows * W * 8 / (XGMI_LINK_GBS * 1e9) * 1e3
+
+
 def arg(name, default):
     return type(default)(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else default
 
 
-out = {"config": cfg_name, "resolution": [W, H], "bands": {}, "allgather_ms": {}, "projected_ms": {},
+gather = sys.argv[sys.argv.index("--gather") + 1] if "--gather" in sys.argv else "peer"
+out = {"config": cfg_name, "resolution": [W, H], "gather": gather, "bands": {}, "allgather_ms": {}, "projected_ms": {},
        "equal_bands": {}, "bounds": {}, "overhead_ms": arg("--overhead-ms", 0.0)}
 only = arg("--only", 0) or None
 rounds = arg("--balance", 5)
@@ -121,13 +131,18 @@ for n in (1, 2, 4, 8):
         out["bounds"][n] = [int(v) for v in bounds]
         worst = max(times)
     out["bands"][n] = round(worst, 4)
-    g = allgather_ms(n)
+    if gather == "ring":
+        g = allgather_ms(n)
+    elif n == 1 or stripes:
+        g = peer_gather_ms(n, stripe_gather_rows(n, H)[0] if n > 1 else H)
+    else:
+        g = peer_gather_ms(n, max(b - a for a, b in zip(bounds[:-1], bounds[1:])))
     ov = out["overhead_ms"] if n > 1 else 0.0
     out["allgather_ms"][n] = round(g, 4)
     out["projected_ms"][n] = {"overlapped": round(max(worst, g) + ov, 4), "serial": round(worst + g + ov, 4)}
     base = out["bands"].get(1)
     speedup = (f"  speedup {base / (max(worst, g) + ov):.2f}x overlapped, {base / (worst + g + ov):.2f}x serial"
                if base else "")
-    print(f"N={n}: slowest band {worst:.4f} ms/frame, all-gather {g:.4f} ms, collective-path overhead {ov:.4f} ms"
+    print(f"N={n}: slowest band {worst:.4f} ms/frame, {gather} gather {g:.4f} ms, collective-path overhead {ov:.4f} ms"
           f"{speedup}", flush=True)
 print(json.dumps(out))
