@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 GPU call: the traverse_top walk with one set of current-walk registers (no per-iteration selects between
-# TLAS and BLAS state; default build) against the select form (exp_lib/libhk_base.so, -DHK_WALK_SELECT=1): the reciprocal self-test, parity
-# suites, bench lines of both on one box.  usage (GPU box): bash tools/r04_c11.sh <tag>
+# Round-4 GPU call: branch-light reciprocals (one rare-path region per inv()) and a triangle test without early
+# returns (default build) against the previous build (exp_lib/libhk_base.so): the reciprocal self-test, parity
+# suites, bench lines of both on one box.  usage (GPU box): bash profiles/r04/scripts/c10.sh <tag>
 set -e
-TAG=${1:-c11}
+TAG=${1:-c10}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 LIB=$R/exp_lib/libhk_base.so
@@ -11,4 +11,4 @@ TESTS="tests/test_gpu_parity.py tests/test_gpu_motion.py tests/test_gpu_wavefron
   bash tools/check_run.sh $TAG cornell:cornell-1080p-nee cornell_base:cornell-1080p-nee:HK_LIB=$LIB \
     city:city-4k city_base:city-4k:HK_LIB=$LIB scene:scene-1080p-full scene_base:scene-1080p-full:HK_LIB=$LIB \
     cornell2:cornell-1080p-nee cornell_base2:cornell-1080p-nee:HK_LIB=$LIB
-echo c11-done
+echo c10-done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU call: spatial reuse's depth window staged with all of a thread's 15 loads in flight (default build)
 # against one load -> wait -> store round trip per texel (exp_lib/libhk_base.so): parity suites, bench lines of both
-# on one box.  usage (GPU box): bash tools/r04_c14.sh <tag>
+# on one box.  usage (GPU box): bash profiles/r04/scripts/c14.sh <tag>
 set -e
 TAG=${1:-c14}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

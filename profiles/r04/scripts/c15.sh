@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU call: spatial reuse at 6 waves per SIMD (exp_lib/libhk_sp6.so, -DHK_SPATIAL_WAVES=6: 78 VGPRs, no
 # spills) against the default 5, and LDS scene staging in every traversal kernel (option lds_scene = 2) on cornell
-# now that staging is cheap.  usage (GPU box): bash tools/r04_c15.sh <tag>
+# now that staging is cheap.  usage (GPU box): bash profiles/r04/scripts/c15.sh <tag>
 set -e
 TAG=${1:-c15}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

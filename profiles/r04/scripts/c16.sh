@@ -2,7 +2,7 @@
 # Round-4 GPU call: the à-trous taps without branches (all 8 taps' loads in flight; default build) against the
 # branchy taps (exp_lib/libhk_base.so, -DHK_DENOISE_BRANCHY=1); the default build also carries spatial reuse's
 # window variant at 6 waves and the fused direct launch's scene staging (measured in c15).  Parity suites, bench
-# lines.  usage (GPU box): bash tools/r04_c16.sh <tag>
+# lines.  usage (GPU box): bash profiles/r04/scripts/c16.sh <tag>
 set -e
 TAG=${1:-c16}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

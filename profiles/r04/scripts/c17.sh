@@ -2,7 +2,7 @@
 # Round-4 GPU call: demodulation with its G-buffer texels read directly and its variance taps selected (default
 # build) against the branchy form (exp_lib/libhk_base.so, -DHK_DEMOD_BRANCHY=1); the default build also carries
 # the c16 build's changes.  Parity suites, bench
-# lines.  usage (GPU box): bash tools/r04_c17.sh <tag>
+# lines.  usage (GPU box): bash profiles/r04/scripts/c17.sh <tag>
 set -e
 TAG=${1:-c17}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: the RCCL path at world size 1 against the single-GPU line at the bench's default step count
-# (cornell, city), and the city 4K band projection with 5 balancing rounds.  usage (GPU box): bash tools/r04_c18.sh <tag>
+# (cornell, city), and the city 4K band projection with 5 balancing rounds.  usage (GPU box): bash profiles/r04/scripts/c18.sh <tag>
 set -e
 TAG=${1:-c18}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: post-change issue / memory-pipe PMC passes (tools/pmc_deep.sh) of the final build, city 4K
-# (spatial reuse, the denoiser) and cornell 1080p (k_indirect).  usage (GPU box): bash tools/r04_c19.sh <tag>
+# (spatial reuse, the denoiser) and cornell 1080p (k_indirect).  usage (GPU box): bash profiles/r04/scripts/c19.sh <tag>
 set -e
 TAG=${1:-c19}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

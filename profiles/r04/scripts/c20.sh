@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU call: the à-trous taps in two batches of four with all of a batch's texel loads issued before the
 # first wait (exp_lib/libhk_pf.so, -DHK_DENOISE_PF=1; branches kept) against the default per-tap loads: parity
-# suites on the experiment build, bench lines of both.  usage (GPU box): bash tools/r04_c20.sh <tag>
+# suites on the experiment build, bench lines of both.  usage (GPU box): bash profiles/r04/scripts/c20.sh <tag>
 set -e
 TAG=${1:-c20}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

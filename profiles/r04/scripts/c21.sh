@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: the committed tree as the driver runs it at round end — the GPU suite, smoke() and the default
-# bench line.  usage (GPU box): bash tools/r04_c21.sh <tag>
+# bench line.  usage (GPU box): bash profiles/r04/scripts/c21.sh <tag>
 set -e
 TAG=${1:-c21}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

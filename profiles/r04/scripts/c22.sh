@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: the separate direct_lit / emissive launches (orbiting camera: the fused launch needs identity
-# reprojection) with the scene staged in LDS (option lds_scene = 2) against the default.  usage: bash tools/r04_c22.sh <tag>
+# reprojection) with the scene staged in LDS (option lds_scene = 2) against the default.  usage: bash profiles/r04/scripts/c22.sh <tag>
 set -e
 TAG=${1:-c22}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: the separate direct_lit / emissive launches staging the scene by default — the GPU suite, the
-# orbiting-camera and 256x256 lines, the default line.  usage (GPU box): bash tools/r04_c23.sh <tag>
+# orbiting-camera and 256x256 lines, the default line.  usage (GPU box): bash profiles/r04/scripts/c23.sh <tag>
 set -e
 TAG=${1:-c23}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: the separate direct launches staging the scene only on frames of >= direct_w4_min_px pixels —
-# the orbiting-camera and 256x256 lines, the forced-variant and motion parity tests.  usage: bash tools/r04_c24.sh <tag>
+# the orbiting-camera and 256x256 lines, the forced-variant and motion parity tests.  usage: bash profiles/r04/scripts/c24.sh <tag>
 set -e
 TAG=${1:-c24}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU call: runtime tests, the default lines against this round's variants, the experiment libraries
 # (spatial reuse: view plane 0 staged in LDS, view planes as one line per pixel), the balanced-band
-# projection of city 4K and a 2-rank rehearsal of its balanced bands.  usage (GPU box): bash tools/r04_c3.sh <tag>
+# projection of city 4K and a 2-rank rehearsal of its balanced bands.  usage (GPU box): bash profiles/r04/scripts/c3.sh <tag>
 set -e
 TAG=${1:-c3}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

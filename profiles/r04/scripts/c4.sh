@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU call: where the collective path's cost at world size 1 goes (cornell 1080p: the band copy, the
 # all-gather, the stripe reorder, the hardware-queue count), a kernel trace of that run, and the balanced
-# city 4K band projection with 3 calibration rounds.  usage (GPU box): bash tools/r04_c4.sh <tag>
+# city 4K band projection with 3 calibration rounds.  usage (GPU box): bash profiles/r04/scripts/c4.sh <tag>
 set -e
 TAG=${1:-c4}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

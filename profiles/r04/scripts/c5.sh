@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU call: the collective path at world size 1 after the row-copy reassembly (cornell stripes,
 # scene / city bands), against the single-GPU lines on the same box; 2-rank rehearsals (gloo, one GPU) of the
-# stripe and balanced-band paths.  usage (GPU box): bash tools/r04_c5.sh <tag>
+# stripe and balanced-band paths.  usage (GPU box): bash profiles/r04/scripts/c5.sh <tag>
 set -e
 TAG=${1:-c5}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

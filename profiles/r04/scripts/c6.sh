@@ -2,7 +2,7 @@
 # Round-4 GPU call: per-channel band windows (direct / emissive launch on core +-16 without emissive spatial
 # reuse) — band parity tests, then the balanced band projections with the measured world-1 collective-path
 # overheads of c5; scene spatial reuse HBM traffic with and without the view planes.
-# usage (GPU box): bash tools/r04_c6.sh <tag>
+# usage (GPU box): bash profiles/r04/scripts/c6.sh <tag>
 set -e
 TAG=${1:-c6}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -2,7 +2,7 @@
 # Round-4 GPU call: k_indirect's temporal tail with the previous record read in two steps (default build) and,
 # in the experiment build exp_lib/libhk_reload.so (-DHK_EXP_RELOAD=2), the pixel's G-buffer / noise fields read
 # again after the walks (105 -> 94 VGPRs, 5 waves per SIMD): parity suites on the experiment build, bench lines
-# of both.  usage (GPU box): bash tools/r04_c7.sh <tag>
+# of both.  usage (GPU box): bash profiles/r04/scripts/c7.sh <tag>
 set -e
 TAG=${1:-c7}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU call: k_indirect forced to 6 waves per SIMD (exp_lib/libhk_w6.so, -DHK_INDIRECT_WAVES=6: 80 VGPRs
-# with 25 spilled) against the default 5-wave build.  usage (GPU box): bash tools/r04_c8.sh <tag>
+# with 25 spilled) against the default 5-wave build.  usage (GPU box): bash profiles/r04/scripts/c8.sh <tag>
 set -e
 TAG=${1:-c8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

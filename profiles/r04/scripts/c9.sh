@@ -2,7 +2,7 @@
 # Round-4 GPU call: the direct passes' previous reservoir read in two steps (default build: fused w4 113/115 -> 97/99
 # VGPRs) and, in exp_lib/libhk_resurf.so (-DHK_EXP_RESURF=1), the emissive pass fetching its surface itself instead
 # of holding the direct pass's through its walks (93/95 VGPRs: 5 waves per SIMD).  Parity suites on the experiment
-# build (it contains both changes), bench lines of both.  usage (GPU box): bash tools/r04_c9.sh <tag>
+# build (it contains both changes), bench lines of both.  usage (GPU box): bash profiles/r04/scripts/c9.sh <tag>
 set -e
 TAG=${1:-c9}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
