@@ -1985,10 +1985,24 @@ HKD f3 dn_rgb(int ch, uint4 rgb, uint2 bi)
     return mk3(unpack_lo16float(rgb.w), unpack_hi16float(rgb.w), unpack_lo16float(bi.x));
 }
 
+// The 3x3 variance blur's taps (denoise.wgsl:116-132) lie within 1 px of the pixel (nearest_texel of uv +- 1 / s is
+// the neighbour, clamped into the frame), so each workgroup stages its 16x16 tile + 1 px of the channels' variance
+// planes in LDS once (the values the taps would load: the same plane index) and the 27 taps of a pixel read LDS.
 template <int C>
 __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
 {
+    constexpr int32_t RW = 18, RS = 24;  // region width (tile + 1 px each side), row stride (an odd multiple of 8)
+    __shared__ float s_var[C][RW * RS];
     const Frame& F = A.F;
+    int32_t x0, y0;
+    tile_origin<XCD_RASTER>(F, F.s_row0, x0, y0);
+    for (int32_t k = (int32_t)threadIdx.x; k < RW * RW; k += 256) {
+        const int32_t ry = k / RW, rx = k - ry * RW;
+        const int32_t vidx = rb_index(F, min(max(x0 - 1 + rx, 0), (int32_t)F.s[0] - 1), min(max(y0 - 1 + ry, 0), (int32_t)F.s[1] - 1));
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) s_var[ch][ry * RS + rx] = D.variance[ch][vidx];
+    }
+    __syncthreads();
     int32_t x, y;
     if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
     const int32_t idx = s_index(F, x, y);
@@ -2026,7 +2040,7 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
             // every tap read (nearest_texel clamps an outside tap into the frame), its term selected
             int32_t vx, vy;
             nearest_texel(suv, F.s, vx, vy);
-            const float v = D.variance[ch][s_index(F, vx, vy)];
+            const float v = s_var[ch][(vy - y0 + 1) * RS + (vx - x0 + 1)];
             const float t = sum_variance + KERNEL3[oy + 1][ox + 1] * fmaxf(v, 0.0f);
             sum_variance = (uv_outside(suv) || v > HK_F32_MAX) ? sum_variance : t;
         }
