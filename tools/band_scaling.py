@@ -19,7 +19,8 @@ printed beside it.  --overhead-ms X adds the measured per-frame cost of the coll
 band copy, the all-gather's stream waits and the reorder at world size 1: HK_BENCH_DIST=1 minus the
 single-GPU line) to every N > 1 frame.
 usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N] [--balance R] [--overhead-ms X]
-                                   [--gather peer|ring]"""
+                                   [--gather peer|ring] [--opts key=value,...]
+--opts: runtime options (hk_set_option) of every band's renderer, for A/B runs."""
 import json
 import sys
 import time
@@ -67,12 +68,13 @@ out = {"config": cfg_name, "resolution": [W, H], "gather": gather, "bands": {}, 
        "equal_bands": {}, "bounds": {}, "overhead_ms": arg("--overhead-ms", 0.0)}
 only = arg("--only", 0) or None
 rounds = arg("--balance", 5)
+opts = {k: float(v) for k, v in (kv.split("=") for kv in arg("--opts", "").split(",") if kv)}
 
 
 def rank_ms(n, rank, stripes, bounds):
     """ms/frame of rank `rank`'s rows of an N-way split, alone on the GPU."""
     if True:
-        r = HikariRenderer(0)
+        r = HikariRenderer(0, opts)
         r.set_noise()
         r.upload_scene(scene)
         r.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
