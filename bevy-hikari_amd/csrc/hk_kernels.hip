@@ -2055,38 +2055,60 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
     if (C == 3) D.den2[idx] = den[2];
 }
 
-// One a-trous level (denoise.wgsl:215-319) with its inputs staged in LDS.  A workgroup's 16x16 tile reads its taps
-// from the tile grown by the level's step on every side ((16 + 2 step)^2 texels: 4x the tile at step 8, 1.27x at
-// step 1); the workgroup copies that region once — each texel's (normal, depth), packed channels and instance,
-// three coalesced 16 / 16 / 8-byte loads — and the taps then read LDS instead of gathering ~37 scattered texels
-// per pixel through the caches.  Every value is the one a per-tap load would read (rb_index of the same
-// coordinates) and the arithmetic per tap is the reference's, so the stored bits are those of the per-tap
-// version: city 4K 0.417 -> 0.354 ms per level (profiles/r05/c3).  Row stride: an odd multiple of 8 texels, so the
-// two 8-texel rows of a 16-lane LDS read phase fall in different halves of the banks.
+// One a-trous level (denoise.wgsl:215-319) with its inputs staged in LDS.  A workgroup's 256 pixels read their taps
+// from a region around them that the workgroup copies once — each texel's (normal, depth), packed channels and
+// instance, three coalesced 16 / 16 / 8-byte loads — and the taps then read LDS instead of gathering ~37 scattered
+// texels per pixel through the caches.  Every value is the one a per-tap load would read (rb_index of the same
+// coordinates) and the arithmetic per tap is the reference's, so the stored bits are those of the per-tap version:
+// city 4K 0.417 -> 0.354 ms per level (profiles/r05/c3).
+// The tile: TW columns x TH rows spaced RSP apart.  A level's taps are `step` px away, so at RSP = step a tile of
+// rows y, y + step, ... reads only rows of its own residue class: the region is (TW + 2 step) x (TH + 2) texels.
+// L0-L2 use 32 x 8 tiles at RSP = step (L0: 48 x 10 texels = 1.9x the tile instead of 32 x 32 = 4x for a 16x16
+// tile; L1 1.6x instead of 2.25x; L2 1.4x instead of 1.6x) and L3 (step 1) a 16x16 tile (1.27x).  Row stride: an
+// odd multiple of 8 texels, so the two 8-texel rows of a 16-lane LDS read phase fall in different halves of the
+// banks.
 template <int LEVEL>
 struct DnRegion {
     static constexpr int32_t step = 8 >> LEVEL;
-    static constexpr int32_t W = 16 + 2 * step;                        // region width = height
-    static constexpr int32_t STRIDE = (W % 16 == 8) ? W : (W / 16) * 16 + (W % 16 < 8 ? 8 : 24);
-    static constexpr int32_t N = W * STRIDE;
+    static constexpr int32_t RSP = LEVEL < 3 ? step : 1;       // row spacing of the tile's pixels
+    static constexpr int32_t TW = LEVEL < 3 ? 32 : 16;          // tile columns
+    static constexpr int32_t TH = 256 / TW;                     // tile rows
+    static constexpr int32_t RW = TW + 2 * step;                // region width
+    static constexpr int32_t RH = TH + 2 * (step / RSP);        // region rows
+    static constexpr int32_t STRIDE = (RW % 16 == 8) ? RW : (RW / 16) * 16 + (RW % 16 < 8 ? 8 : 24);
+    static constexpr int32_t N = RH * STRIDE;
 };
+template <int LEVEL>
+static dim3 level_tiles(uint32_t width, int32_t rows)
+{
+    using R = DnRegion<LEVEL>;
+    const uint32_t block = (uint32_t)(R::TH * R::RSP);  // rows of one block of RSP tiles
+    return dim3((width + R::TW - 1u) / R::TW, ((uint32_t)rows + block - 1u) / block * R::RSP, 1);
+}
 template <int C, int LEVEL>
 __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 {
     using R = DnRegion<LEVEL>;
-    constexpr int32_t step = R::step;
+    constexpr int32_t step = R::step, rstep = step / R::RSP;  // a tap's offset in region columns / rows
     __shared__ float4 s_nd[R::N];
     __shared__ uint4 s_rgb[R::N];
     __shared__ uint2 s_bi[R::N];
     const Frame& F = A.F;
-    int32_t x0, y0;
-    tile_origin<DENOISE_ORDER>(F, F.s_row0, x0, y0);
+    uint32_t tx, ty;
+    tile_coords<DENOISE_ORDER>(tx, ty);
+    const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0;
+    const int32_t w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : F.s_rows;
+    const int32_t x0 = (int32_t)tx * R::TW;
+    // band row of the tile's first row: block ty / RSP, residue ty % RSP
+    const int32_t ly0 = w0 + (int32_t)(ty / R::RSP) * R::TH * R::RSP + (int32_t)(ty % R::RSP);
     {
-        const int32_t rx0 = x0 - step, ry0 = y0 - step;
-        for (int32_t k = (int32_t)threadIdx.x; k < R::W * R::W; k += 256) {
-            const int32_t ry = k / R::W, rx = k - ry * R::W;
+        const int32_t y0 = F.s_row0 + ly0;
+        for (int32_t k = (int32_t)threadIdx.x; k < R::RW * R::RH; k += 256) {
+            const int32_t ry = k / R::RW, rx = k - ry * R::RW;
             // out-of-frame texels are never tapped (the tap bounds test below); read at clamped coordinates
-            const int32_t sidx = rb_index(F, min(max(rx0 + rx, 0), (int32_t)F.s[0] - 1), min(max(ry0 + ry, 0), (int32_t)F.s[1] - 1));
+            const int32_t gx = min(max(x0 - step + rx, 0), (int32_t)F.s[0] - 1);
+            const int32_t gy = min(max(y0 + (ry - rstep) * R::RSP, 0), (int32_t)F.s[1] - 1);
+            const int32_t sidx = rb_index(F, gx, gy);
             const float4 nd = D.nd[sidx];
             const uint4 rgb = D.rgb[LEVEL][sidx];
             const uint2 bi = D.bi[LEVEL][sidx];
@@ -2098,9 +2120,21 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
     }
     __syncthreads();
     int32_t x, y;
-    if (!tile_pixel<DENOISE_ORDER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    int32_t tc, tr;  // the pixel's tile column / row
+    if constexpr (R::TW == 16) {  // 16x16: a wave per 8x8 quad (tile_pixel_at)
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+        tc = (int32_t)((w & 1u) * 8u + (lane & 7u));
+        tr = (int32_t)((w >> 1) * 8u + (lane >> 3));
+    } else {
+        tc = (int32_t)(threadIdx.x % R::TW);
+        tr = (int32_t)(threadIdx.x / R::TW);
+    }
+    x = x0 + tc;
+    const int32_t ly = ly0 + tr * R::RSP;
+    if (x >= (int32_t)F.s[0] || ly >= w1) return;
+    y = global_row(F, ly, F.s_row0);
     const int32_t idx = rb_index(F, x, y);
-    const int32_t oc = (y - y0 + step) * R::STRIDE + (x - x0 + step);  // the pixel in the region
+    const int32_t oc = (tr + rstep) * R::STRIDE + (tc + step);  // the pixel in the region
     const float4 g0 = s_nd[oc];
     const uint2 cbi = s_bi[oc];
     const float depth = g0.w;
@@ -2143,7 +2177,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
         // uv_outside(coords_to_uv(s)) exactly: (sx + 0.5) / w < 0 iff sx < 0, and its rounding
         // exceeds 1 iff sx >= w (for w < 2^24 the quotient is >= 1 + 2^-13 or <= 1 - 2^-25)
         if (sx < 0 || sy < 0 || sx >= (int32_t)F.s[0] || sy >= (int32_t)F.s[1]) continue;
-        const int32_t o = oc + oy * step * R::STRIDE + ox * step;
+        const int32_t o = oc + oy * rstep * R::STRIDE + ox * step;
         const float4 t0 = s_nd[o];
         const uint4 trgb = s_rgb[o];
         const uint2 tbi = s_bi[o];
@@ -2477,21 +2511,26 @@ void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
     if (D.channels == 3) hipLaunchKernelGGL(k_demod3<3>, g, dim3(256), 0, st, A, D);
     else hipLaunchKernelGGL(k_demod3<2>, g, dim3(256), 0, st, A, D);
 }
+template <int C, int LEVEL>
+static void launch_level(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
+{
+    const dim3 g = level_tiles<LEVEL>(A.F.s[0], A.F.win_rows > 0 ? A.F.win_rows : A.F.s_rows);
+    hipLaunchKernelGGL((k_denoise3<C, LEVEL>), g, dim3(256), 0, st, A, D);
+}
 template <int C>
-static void launch_level(const FrameArgs& A, const DenoiseArgs& D, int level, dim3 g, hipStream_t st)
+static void launch_level(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st)
 {
     switch (level) {
-    case 0: hipLaunchKernelGGL((k_denoise3<C, 0>), g, dim3(256), 0, st, A, D); break;
-    case 1: hipLaunchKernelGGL((k_denoise3<C, 1>), g, dim3(256), 0, st, A, D); break;
-    case 2: hipLaunchKernelGGL((k_denoise3<C, 2>), g, dim3(256), 0, st, A, D); break;
-    default: hipLaunchKernelGGL((k_denoise3<C, 3>), g, dim3(256), 0, st, A, D); break;
+    case 0: launch_level<C, 0>(A, D, st); break;
+    case 1: launch_level<C, 1>(A, D, st); break;
+    case 2: launch_level<C, 2>(A, D, st); break;
+    default: launch_level<C, 3>(A, D, st); break;
     }
 }
 void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStream_t st)
 {
-    dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
-    if (D.channels == 3) launch_level<3>(A, D, level, g, st);
-    else launch_level<2>(A, D, level, g, st);
+    if (D.channels == 3) launch_level<3>(A, D, level, st);
+    else launch_level<2>(A, D, level, st);
 }
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {
