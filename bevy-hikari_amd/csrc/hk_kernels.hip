@@ -155,10 +155,11 @@ __global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V, uint2*
 {
     // The traversal stack's LDS levels, in the launch's dynamic LDS (entry-major, [level][256]): every
     // level of the scene's stack bound for SHALLOW (launch_gbuffer sizes it: a shallow scene's
-    // workgroups then take less LDS and more of them fit a CU), the first LVL otherwise; the
-    // scene-staged variant keeps the whole stack in scratch so that scene + stack stay within the LDS
-    // budget.
-    uint2* const gb_lds_stack = LDS ? nullptr : reinterpret_cast<uint2*>(hk_lds_scene);
+    // workgroups then take less LDS and more of them fit a CU), the first LVL otherwise.  The
+    // scene-staged variant (LDS) puts a shallow scene's stack after the staged arrays (small frames:
+    // launch_gbuffer) and a deep one in scratch.
+    uint2* gb_lds_stack = reinterpret_cast<uint2*>(hk_lds_scene);
+    if constexpr (LDS) gb_lds_stack = SHALLOW ? reinterpret_cast<uint2*>(hk_lds_scene + stage_bytes(A.sc.bytes, PLAN_GBUFFER) / 4u) : nullptr;
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_GBUFFER>(A.sc, hk_lds_scene);
     else sc = A.sc;
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V, uint2*
         ray.origin = ld3(V.world_position);
         ray.direction = primary_direction(V, ((float)x + 0.5f) - V.jitter[0], ((float)y + 0.5f) - V.jitter[1], A.F.S);
         ray.inv_direction = inv(ray.direction);
-        Hit hit = closest_hit_ordered<SHALLOW && !LDS, LVL>(sc, ray, LDS ? nullptr : gb_lds_stack);
+        Hit hit = closest_hit_ordered<SHALLOW, LVL>(sc, ray, gb_lds_stack);
         if (hit.instance_index == HK_U32_MAX) {
             // a miss stores constant zeros: skipped when this slot already holds them (V.bg)
             bool stored = false;
@@ -2296,15 +2297,23 @@ static uint32_t lds_plan_bytes(const FrameArgs& A, int plan, bool preferred)
 
 void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32_t stack_need, hipStream_t st)
 {
-    const uint32_t lds = lds_plan_bytes(A, PLAN_GBUFFER, false);
     const dim3 g = tiles(A.F, A.F.S[0], A.F.S_rows);
     constexpr uint32_t level_bytes = 256u * sizeof(uint2);  // one stack level of the workgroup
     // option gbuffer_stack_full: the shallow variant with all GB_STACK_LDS levels (the round-2 allocation)
     const bool full = A.opt.gbuffer_stack_full != 0;
-    if (lds) hipLaunchKernelGGL((k_gbuffer<true, false>), g, dim3(256), lds, st, A, V, albedo);
-    else if (stack_need <= (uint32_t)GB_STACK_LDS && !A.opt.gbuffer_deep) {
+    const bool shallow = stack_need <= (uint32_t)GB_STACK_LDS && !A.opt.gbuffer_deep;
+    const uint32_t levels = full ? (uint32_t)GB_STACK_LDS : (stack_need ? stack_need : 1u);
+    // A small frame (an 8- or 4-way stripe of 1080p: <= gbuffer_lds_max_px pixels, one dispatch round) is as long
+    // as one wave's walk, a chain of dependent node loads: there the scene is staged in LDS with the stack after it
+    // (cornell 8-way stripe ...).  A whole frame runs many rounds and stays on L2 node loads (round 1: even).
+    const bool small = (double)A.F.S[0] * (double)(A.F.win_rows > 0 ? A.F.win_rows : A.F.S_rows) <= A.opt.gbuffer_lds_max_px;
+    const uint32_t scene = lds_plan_bytes(A, PLAN_GBUFFER, small);
+    // (scene + stack within the LDS budget of a staged kernel)
+    if (scene && shallow && scene + levels * level_bytes <= LDS_SCENE_MAX + 16384u)
+        hipLaunchKernelGGL((k_gbuffer<true, true>), g, dim3(256), scene + levels * level_bytes, st, A, V, albedo);
+    else if (scene) hipLaunchKernelGGL((k_gbuffer<true, false, 0>), g, dim3(256), scene, st, A, V, albedo);
+    else if (shallow) {
         // pushes never exceed the bound (hk_runtime gb_stack_need: inner nodes on a TLAS + BLAS path)
-        const uint32_t levels = full ? (uint32_t)GB_STACK_LDS : (stack_need ? stack_need : 1u);
         hipLaunchKernelGGL((k_gbuffer<false, true>), g, dim3(256), levels * level_bytes, st, A, V, albedo);
     } else {
         // a deep scene: GB_DEEP_LDS levels in LDS, the rest in scratch (8 levels: 16 KiB per workgroup,

@@ -16,6 +16,7 @@ struct LaunchOpts {
     int lds_scene = 1;               // ("lds_scene") 0: no LDS scene staging, 1: where it measured faster, 2: every traversal kernel
     int gbuffer_stack_full = 0;      // ("gbuffer_stack_full") shallow G-buffer walk with all GB_STACK_LDS levels
     int gbuffer_deep = 0;            // ("gbuffer_deep") the deep-scene G-buffer variant on any scene
+    double gbuffer_lds_max_px = 6e5; // ("gbuffer_lds_max_px") G-buffer with the scene and its stack in LDS up to this many pixels
     double direct_w4_min_px = 4e5;   // ("direct_w4_min_px") k_direct_lit_w4 from this many pixels up
     int fused_w4 = 1;                // ("fused_w4") the 4-wave fused direct/emissive variants
     int persistent_indirect = 0;     // ("persistent_indirect") k_indirect_persist (opt-in, measured slower)

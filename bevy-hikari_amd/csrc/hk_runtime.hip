@@ -53,6 +53,7 @@ enum Opt {
     OPT_LDS_SCENE,           // LaunchOpts
     OPT_GBUFFER_STACK_FULL,
     OPT_GBUFFER_DEEP,
+    OPT_GBUFFER_LDS_MAX_PX,
     OPT_DIRECT_W4_MIN_PX,
     OPT_FUSED_W4,
     OPT_PERSISTENT_INDIRECT,
@@ -70,6 +71,7 @@ constexpr OptDef OPTS[OPT_COUNT] = {
     {"merge", -1, -1, 1},                  {"bg_elision", 1, 0, 1},        {"spatial_view_planes", 1, 0, 1},
     {"band_full_windows", 0, 0, 1},        {"leaf_collapse", 1, 0, 1},     {"gbuffer_reuse", 1, 0, 1},
     {"lds_scene", 1, 0, 2},                {"gbuffer_stack_full", 0, 0, 1}, {"gbuffer_deep", 0, 0, 1},
+    {"gbuffer_lds_max_px", 6e5, 0.0, 1e12},
     {"direct_w4_min_px", 4e5, 0.0, 1e12},  {"fused_w4", 1, 0, 1},          {"persistent_indirect", 0, 0, 1},
     {"compact_emitter", 0, 0, 1},          {"compact_shadow", 0, 0, 1},
 };
@@ -641,6 +643,7 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     A.opt.lds_scene = (int)c->opt[OPT_LDS_SCENE];
     A.opt.gbuffer_stack_full = c->on(OPT_GBUFFER_STACK_FULL);
     A.opt.gbuffer_deep = c->on(OPT_GBUFFER_DEEP);
+    A.opt.gbuffer_lds_max_px = c->opt[OPT_GBUFFER_LDS_MAX_PX];
     A.opt.direct_w4_min_px = c->opt[OPT_DIRECT_W4_MIN_PX];
     A.opt.fused_w4 = c->on(OPT_FUSED_W4);
     A.opt.persistent_indirect = c->on(OPT_PERSISTENT_INDIRECT);
@@ -879,7 +882,7 @@ int hk_set_option(hk_ctx* c, const char* key, double value)
         if (!(value >= OPTS[k].lo && value <= OPTS[k].hi))
             return fail(c, HK_ERR_INVALID, std::string("option ") + key + " out of range");
         // every key but the pixel-count thresholds is an on/off switch or a mode: integers only
-        if (!std::strstr(key, "_min_px") && value != std::floor(value))
+        if (!std::strstr(key, "_px") && value != std::floor(value))
             return fail(c, HK_ERR_INVALID, std::string("option ") + key + " takes an integer value");
         c->opt[k] = value;
         c->gen++;  // (G-buffer reuse: planes written under other options are not reused)

@@ -215,14 +215,15 @@ void hk_settings_default(hk_settings* out);
  *   gbuffer_reuse (1)        skip the G-buffer trace when its slot already holds this frame's planes
  *                            (static camera, jitter and instances: the sub-frames of an accumulation)
  *   lds_scene (1)            0 no LDS scene staging, 1 where measured faster, 2 every traversal kernel
- *   gbuffer_stack_full (0), gbuffer_deep (0), direct_w4_min_px (4e5), fused_w4 (1),
+ *   gbuffer_stack_full (0), gbuffer_deep (0), gbuffer_lds_max_px (6e5: scene + stack in LDS on smaller
+ *   frames), direct_w4_min_px (4e5), fused_w4 (1),
  *   persistent_indirect (0)  kernel-variant choices (tests force each variant with them)
  *   compact_emitter (0)      the fused direct/emissive launch runs a workgroup's emitter BLAS walks as one
  *                            compacted batch (long walks first) on frames without emissive validation
  *   compact_shadow (0)       shadow walks of a workgroup as one compacted batch (fused launch, indirect pass)
  *                            (both measured slower than the per-pixel walks: DESIGN §4)
  * hk_set_option returns HK_ERR_INVALID for an unknown key, a value outside the key's range, or a fractional value
- * for any key but the *_min_px thresholds. */
+ * for any key but the pixel-count thresholds (*_px). */
 int hk_set_option(hk_ctx* ctx, const char* key, double value);
 int hk_get_option(const hk_ctx* ctx, const char* key, double* value);
 /* key of option `index` (0, 1, ...; NULL past the last one) */

@@ -68,7 +68,9 @@ out = {"config": cfg_name, "resolution": [W, H], "gather": gather, "bands": {}, 
        "equal_bands": {}, "bounds": {}, "overhead_ms": arg("--overhead-ms", 0.0)}
 only = arg("--only", 0) or None
 rounds = arg("--balance", 5)
-opts = {k: float(v) for k, v in (kv.split("=") for kv in arg("--opts", "").split(",") if kv)}
+# bench.py's options: the G-buffer is rendered every frame at 1 spp (gbuffer_reuse would skip it on a static camera)
+opts = {"gbuffer_reuse": 1 if cfg.get("spp", 1) > 1 else 0,
+        **{k: float(v) for k, v in (kv.split("=") for kv in arg("--opts", "").split(",") if kv)}}
 
 
 def rank_ms(n, rank, stripes, bounds):
