@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(256) void k_indirect_persist(FrameArgs A, ChannelAr
 // The fused direct/emissive pass and the one-bounce indirect pass in ONE launch.  They read the same
 // G-buffer and write disjoint buffers (reservoirs 0-5 and the direct / emissive planes, reservoirs 6-9
 // and the indirect planes: light.rs:518-546), so their workgroups are independent and are interleaved
-// in one grid — blockIdx.z 0: an indirect tile, 1: the direct tile — instead of the indirect pass
+// in one grid — blockIdx.z 0: a direct tile, 1: the indirect tile — instead of the indirect pass
 // running on a side stream joined by events.  Each CU then mixes both kinds of work and the frame has
 // no cross-stream dependency: cornell 8-way stripe ....  Same per-pixel code as
 // k_direct_fused_w4 / k_indirect, so the results are identical.  The direct role parks its validation
@@ -1398,13 +1398,13 @@ template <bool VD, bool VE, bool LDS_I>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_light_merged(FrameArgs A, ChannelArgs C0,
                                                                                                 ChannelArgs C1, ChannelArgs C2)
 {
-    // gridDim.z == 2: every indirect workgroup (z = 0) is dispatched before the direct ones
+    // gridDim.z == 2: every direct workgroup (z = 0) is dispatched before the indirect ones
     const bool zsplit = gridDim.z == 2u;
     const uint32_t bx = zsplit ? blockIdx.x : blockIdx.x >> 1, gx = zsplit ? gridDim.x : gridDim.x >> 1;
     int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
     const bool active = tile_pixel_at<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, bx, blockIdx.y, gx, gridDim.y, x, y);
-    if (zsplit ? blockIdx.z == 0u : (blockIdx.x & 1u) != 0u) {
+    if (zsplit ? blockIdx.z == 1u : (blockIdx.x & 1u) != 0u) {
         Scene sc = A.sc;
         if constexpr (LDS_I) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
         if (active) indirect_body<false>(A, sc, C2, x, y, n_top, n_emitter);
@@ -2466,8 +2466,9 @@ void launch_light_merged(const FrameArgs& A, const ChannelArgs& C0, const Channe
                          hipStream_t st)
 {
     dim3 g = tiles(A.F, A.F.s[0], A.F.s_rows);
-    // the indirect workgroups, which live longer, are dispatched first (grid z 0, then the direct ones at
-    // z 1): cornell 8-way stripe 0.1194 -> 0.1181 ms/frame against even / odd blockIdx.x
+    // the direct workgroups are dispatched first (grid z 0, then the indirect ones at z 1): cornell 4-way stripe
+    // 0.1453 -> 0.1412 ms/frame, 2- and 8-way even, against the indirect ones first (round 3's order, then 8-way
+    // 0.1194 -> 0.1181 against even / odd blockIdx.x; profiles/r05/c16, c18)
     g.z = 2u;
     const uint32_t scene = lds_plan_bytes(A, PLAN_LIGHT, true);
     const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
