@@ -39,6 +39,7 @@ struct TimedLaunch {
 // variables on the frame path); the defaults are the measured-fastest configuration.
 enum Opt {
     OPT_PIPELINE_MIN_PX,     // frame pipelining (G-buffer / tail streams) from this many integrator pixels up
+    OPT_PIPELINE_HEAVY_MIN_PX,  // ... and from this many up on frames with spatial reuse or the denoiser
     OPT_GBUFFER_PIPELINE,    // k_gbuffer of frame f on its own stream next to frame f-1's light passes
     OPT_TAIL_PIPELINE,       // denoise + tone-sum of frame f on their own stream next to frame f+1
     OPT_CHANNEL_STREAMS,     // the indirect chain on a side stream next to direct -> emissive
@@ -66,7 +67,7 @@ struct OptDef {
     double def, lo, hi;
 };
 constexpr OptDef OPTS[OPT_COUNT] = {
-    {"pipeline_min_px", 1.2e6, 0.0, 1e12}, {"gbuffer_pipeline", 1, 0, 1},  {"tail_pipeline", 1, 0, 1},
+    {"pipeline_min_px", 1.2e6, 0.0, 1e12}, {"pipeline_heavy_min_px", 0.0, 0.0, 1e12}, {"gbuffer_pipeline", 1, 0, 1},  {"tail_pipeline", 1, 0, 1},
     {"channel_streams", 1, 0, 1},          {"fuse", 1, 0, 1},              {"fuse_min_px", 1048576.0, 0.0, 1e12},
     {"merge", -1, -1, 1},                  {"bg_elision", 1, 0, 1},        {"spatial_view_planes", 1, 0, 1},
     {"band_full_windows", 0, 0, 1},        {"leaf_collapse", 1, 0, 1},     {"gbuffer_reuse", 1, 0, 1},
@@ -92,6 +93,8 @@ struct hk_ctx {
     float4* blas_wide = nullptr;  // G-buffer traversal layout (k_build_wide)
     float4* tlas_wide = nullptr;
     uint32_t gb_stack_need = 0;   // TLAS + BLAS subtree depth bound of closest_hit_ordered
+    bool heavy = false;           // the last hk_render_frame had spatial reuse or followed a denoised frame (pipeline_size)
+    int dn_calls = 0;             // hk_denoise calls since the last hk_render_frame
     uint32_t gb_blas_depth = 0;   // BLAS part of it (the TLAS part changes with hk_update_instances)
     void* dyn_scratch = nullptr;  // hk_update_instances scratch (sized at upload)
     size_t dyn_bytes = 0;
@@ -351,12 +354,17 @@ int tail_end(hk_ctx* c)
     c->dn_pending = true;
     return HK_OK;
 }
-// Frame pipelining pays on large frames only: on a small band or stripe (a 2- to 8-way split of
-// 1080p: <= 1 Mpx, 0.15-0.35 ms frames) the cross-stream waits cost more than the overlap hides
-// (cornell 8-way stripe 0.145 -> 0.172 ms), on a 1080p frame or a 4K band it gains.
+// Frame pipelining pays on large frames: on a small stripe of traversal + NEE alone (a 2- to 8-way split
+// of 1080p: <= 1 Mpx, 0.1-0.25 ms frames) the cross-stream waits cost more than the overlap hides
+// (cornell 8-way stripe 0.145 -> 0.172 ms), on a 1080p frame or a 4K band it gains.  A frame with spatial
+// reuse or the denoiser (`heavy`: this frame's spatial settings, or hk_denoise in the previous frame) has a
+// long G-buffer and tail to hide, and pipelines at every size: scene 1080p 2-way band 1.12 -> 0.92 ms,
+// 8-way 0.50 -> 0.45, city 4K 8-way 0.90 -> 0.86 (profiles/r05/c21).  Only the schedule changes, never
+// the results.
 bool pipeline_size(const hk_ctx* c)
 {
-    return (double)c->s[0] * (double)c->s_rows >= c->opt[OPT_PIPELINE_MIN_PX];
+    const double px = (double)c->s[0] * (double)c->s_rows;
+    return px >= c->opt[OPT_PIPELINE_MIN_PX] || (c->heavy && px >= c->opt[OPT_PIPELINE_HEAVY_MIN_PX]);
 }
 bool dn_pipeline_enabled(const hk_ctx* c) { return c->on(OPT_TAIL_PIPELINE) && pipeline_size(c); }
 // the scene, sizes or G-buffer planes change on the caller's stream: the next k_gbuffer must run
@@ -1602,6 +1610,8 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick_frame(c, stream);
+    c->heavy = settings->indirect_spatial_reuse || settings->emissive_spatial_reuse || c->dn_calls > 0;  // pipeline_size
+    c->dn_calls = 0;
     // Frame-tail pipelining: with all three channels rendered, this frame's render / variance
     // targets are the other slot, last read by frame f-2's denoise / tone-sum, so frame f-1's tail
     // (on dn_stream) can still be running while this frame's light passes start.
@@ -1790,6 +1800,7 @@ int hk_denoise(hk_ctx* c, const hk_settings* settings, const hk_frame_inputs* in
     if (!settings || !in) return fail(c, HK_ERR_INVALID, "null settings or frame inputs");
     if (!settings->denoise) return HK_OK;
     if (c->stripe_n >= 2) return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude the denoiser: it reads neighbours");
+    c->dn_calls++;
     (void)hipSetDevice(c->device);
     hipStream_t caller = pick_frame(c, stream);
     // after a slot-swapping hk_render_frame: on dn_stream, next to the following frame's passes

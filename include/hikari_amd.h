@@ -203,6 +203,7 @@ void hk_settings_default(hk_settings* out);
  * depend on them; the defaults are the measured-fastest configuration.  Nothing is read from the
  * environment.  Keys (default):
  *   pipeline_min_px (1.2e6)  frame pipelining from this many integrator pixels up
+ *   pipeline_heavy_min_px (0)  ... and from this many up on frames with spatial reuse or the denoiser
  *   gbuffer_pipeline (1)     frame f's G-buffer on its own stream next to frame f-1's light passes
  *   tail_pipeline (1)        frame f's denoise / tone-sum / accumulation next to frame f+1's light passes
  *   channel_streams (1)      the indirect chain on a side stream next to direct -> emissive
