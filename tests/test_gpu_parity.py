@@ -142,14 +142,20 @@ def test_full_size_bench_workloads_bit_exact(config, frames, uneven):
     assert r.counters() == o.counters()
 
 
-@pytest.mark.parametrize("denoise", [True, False], ids=["denoise", "tone_only"])
-def test_frame_pipelining_bit_exact(hk_options, denoise):
+@pytest.mark.parametrize("denoise,mode", [(True, "forced"), (False, "forced"), (True, "serial")],
+                         ids=["denoise", "tone_only", "denoise_serial"])
+def test_frame_pipelining_bit_exact(hk_options, denoise, mode):
     """Frame pipelining forced on a small frame (option pipeline_min_px=0): the G-buffer of frame f on
     its own stream next to frame f-1's light passes, frame f's tail (denoise, tone-sum) next to
     frame f+1's; every plane, reservoir and counter of every frame as the oracle's serial run,
-    with readbacks after each frame and without (outputs compared after the last frame only)."""
+    with readbacks after each frame and without (outputs compared after the last frame only).
+    (Frames with spatial reuse pipeline at every size by default, pipeline_heavy_min_px = 0; "serial" keeps
+    them in series: pipeline_heavy_min_px above the frame.)"""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
-    hk_options["pipeline_min_px"] = 0
+    if mode == "forced":
+        hk_options["pipeline_min_px"] = 0
+    else:
+        hk_options["pipeline_heavy_min_px"] = 1e12
     w, h = 96, 72
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=denoise)
     scene, cam, lights, r, o = _setup(w, h, st)
@@ -164,6 +170,33 @@ def test_frame_pipelining_bit_exact(hk_options, denoise):
             x.denoise(s, fi)
             x.tone_sum(s)
         if f < 3 or f == frames - 1:  # frames 3..7 run back to back, no readback in between
+            _compare_frame(r, o, f, errors)
+        if errors:
+            break
+    assert not errors, "\n".join(errors[:20])
+    assert r.counters() == o.counters()
+
+
+def test_heavy_frame_schedule_switches_bit_exact(hk_options):
+    """The schedule follows the settings (pipeline_size: a frame with spatial reuse or after a denoised frame
+    pipelines at any size, a frame of traversal + NEE alone below pipeline_min_px does not): a sequence that
+    turns spatial reuse and the denoiser off and on again switches between the pipelined and the serial
+    schedule (and the merged light launch) from frame to frame, and every frame equals the oracle's."""
+    from hikari_amd import HikariSettings, Upscale, frame_inputs
+    w, h = 96, 72
+    heavy = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=True)
+    light = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=False, denoise=False)
+    scene, cam, lights, r, o = _setup(w, h, heavy)
+    errors = []
+    for f, st in enumerate([heavy, heavy, light, light, heavy, light, heavy, heavy]):
+        s = st.to_c()
+        fi = frame_inputs(f, cam, lights, w, h)
+        for x in (r, o):
+            x.render_gbuffer(fi)
+            x.render_frame(s, fi)
+            x.denoise(s, fi)
+            x.tone_sum(s)
+        if f % 2 == 1 or f == 7:
             _compare_frame(r, o, f, errors)
         if errors:
             break
