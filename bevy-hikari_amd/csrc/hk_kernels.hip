@@ -1718,6 +1718,11 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         float sample_depth = win_depth<WINDOW>(F, A.G, W, sdx, sdy);
         float depth_ratio = depth / sample_depth;
         if (depth_ratio < 0.9f || depth_ratio > 1.1f) continue;
+        const int32_t nidx = rb_index(F, scx, scy);
+        // (VIEW) the neighbour's view plane 0 is gathered before the march: the march's LDS and VALU work then
+        // hides the gather's latency (a neighbour the march rejects has read 16 bytes for nothing)
+        uint4 view0 = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (VIEW) view0 = C.view[view_at(C.view_n, 0u, (uint32_t)nidx)];
         // the screen-space depth march first: it reads only the LDS depth window and rejects a third of
         // the neighbours (city 1080p: 35 %; the count / normal and direction tests below reject < 1 %),
         // so those never gather reservoir planes.  The rejection tests are pure, so their order does not
@@ -1754,7 +1759,6 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         // the neighbour's reservoir, its 16-byte planes loaded as the tests need them (the rejection
         // tests read plane 3 (count, normals) and plane 2 (sample position); planes 0-1 only for a
         // neighbour that is merged): the same values as load_res, fewer gathers for rejected ones
-        const int32_t nidx = rb_index(F, scx, scy);
         // the neighbour's record: the view planes (VIEW, store_res_view) or the reservoir's own 16-byte
         // planes, loaded as the tests need them (rejection: plane 3 count / normal, plane 2 sample
         // position; merge: planes 0-1): the same values as load_res either way
@@ -1763,7 +1767,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         bool count_ok;
         f3 q_sample;
         if constexpr (VIEW) {
-            const uint4 a = C.view[view_at(C.view_n, 0u, (uint32_t)nidx)];
+            const uint4 a = view0;
             normal_word = a.w;
             count_ok = (a.w & VIEW_COUNT) != 0u;
             q_sample = mk3(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
