@@ -1052,6 +1052,16 @@ HKD void bounce_hit_b(const Scene& sc, const Frame& F, BounceState& B, bool shad
 // The pass up to the one-bounce path's shadow walk (I.shadow: whether it is traced; the multiple-bounce
 // path runs its whole loop here).  Returns false when the pixel's pass ends here: a background pixel (its
 // stores done), the IND_GEN / IND_TRACE stages (*ret: their result).
+// The pixel's G-buffer and blue-noise fields, kept in LDS through the walks by the tile kernels (k_indirect,
+// k_light_merged): indirect_end reads them back from there instead of from global memory (one thread's slot,
+// struct-of-arrays so that a wave's 16-byte accesses are conflict-free)
+struct IndStash {
+    float4 pd[256];     // position, depth
+    float4 vel[256];    // velocity, uv
+    float4 rnd[256];    // s.random
+    float4 nrm[256];    // normalize(normal), visible instance (bits)
+    uint32_t im_y[256]; // material
+};
 struct IndirectState {
     BounceState B;
     int32_t x, y, idx;
@@ -1063,7 +1073,8 @@ struct IndirectState {
 };
 template <bool MULTI, int STAGE = IND_ALL>
 HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
-                        uint32_t& n_emitter, const WfArgs* W, uint32_t* key, IndirectState& I, bool& ret)
+                        uint32_t& n_emitter, const WfArgs* W, uint32_t* key, IndirectState& I, bool& ret,
+                        IndStash* stash = nullptr)
 {
     static_assert(!MULTI || STAGE == IND_ALL, "the wavefront stages cover one bounce");
     I.shadow = false;
@@ -1108,6 +1119,14 @@ HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& 
     s.visible_position = mk4(position.x, position.y, position.z, depth);
     s.visible_normal = normal;
     s.visible_instance = im_x;
+    if (stash) {
+        const uint32_t t = threadIdx.x;
+        stash->pd[t] = make_float4(pd.x, pd.y, pd.z, pd.w);
+        stash->vel[t] = make_float4(velocity_uv.x, velocity_uv.y, velocity_uv.z, velocity_uv.w);
+        stash->rnd[t] = make_float4(s.random.x, s.random.y, s.random.z, s.random.w);
+        stash->nrm[t] = make_float4(normal.x, normal.y, normal.z, __uint_as_float(im_x));
+        stash->im_y[t] = im_y;
+    }
 
     Ray ray;
     HitInfo info;
@@ -1206,12 +1225,25 @@ HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& 
 }
 // the rest of the pass after the shadow walk (sh: its result when I.shadow)
 template <bool MULTI>
-HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, IndirectState& I, const Hit& sh)
+HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, IndirectState& I, const Hit& sh,
+                      const IndStash* stash = nullptr)
 {
     const Frame& F = A.F;
     if (!MULTI) bounce_hit_b(sc, F, I.B, I.shadow, sh);
     Sample& s = I.B.s;
-    {
+    if (stash) {
+        // the same fields from the thread's LDS slot (indirect_begin wrote them): no global round trip in the tail
+        __asm__ volatile("" ::: "memory");
+        const uint32_t t = threadIdx.x;
+        const float4 pd = stash->pd[t], nv = stash->nrm[t], vel = stash->vel[t], rnd = stash->rnd[t];
+        s.visible_position = mk4(pd.x, pd.y, pd.z, pd.w);
+        s.visible_normal = mk3(nv.x, nv.y, nv.z);
+        s.visible_instance = __float_as_uint(nv.w);
+        s.random = mk4(rnd.x, rnd.y, rnd.z, rnd.w);
+        I.position = mk4(pd.x, pd.y, pd.z, 1.0f);
+        I.velocity_uv = mk4(vel.x, vel.y, vel.z, vel.w);
+        I.im_y = stash->im_y[t];
+    } else {
         // The pixel's G-buffer and blue-noise fields read again here — the same texels, so the same bits — behind
         // a compiler barrier, instead of being held in registers through both walks: with the previous record
         // read in two steps below, the pass's register peak (this tail) falls from 105 to 94 VGPRs, 4 -> 5 waves
@@ -1287,15 +1319,15 @@ HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C,
 // returns (IND_GEN) whether the pixel traces a bounce; (IND_TRACE) the hit's material bin in *key
 template <bool MULTI, int STAGE = IND_ALL>
 HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
-                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr)
+                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr, IndStash* stash = nullptr)
 {
     IndirectState I;
     bool ret;
-    if (!indirect_begin<MULTI, STAGE>(A, sc, C, x, y, n_top, n_emitter, W, key, I, ret)) return ret;
+    if (!indirect_begin<MULTI, STAGE>(A, sc, C, x, y, n_top, n_emitter, W, key, I, ret, stash)) return ret;
     Hit sh;
     if (!MULTI && I.shadow)
         sh = traverse_top(sc, I.B.ray, I.B.cand.max_distance, I.B.cand.min_distance, I.B.cand.emissive_instance);
-    indirect_end<MULTI>(A, sc, C, I, sh);
+    indirect_end<MULTI>(A, sc, C, I, sh, stash);
     return true;
 }
 
@@ -1319,7 +1351,10 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
                           I.B.cand.emissive_instance, sh);
         if (live) indirect_end<false>(A, sc, C, I, sh);
     } else if (active) {
-        indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter);
+        // the pixel's fields through the walks in LDS (IndStash): k_indirect alone city 4K 0.590 -> 0.558 ms, scene
+        // 1080p 0.268 -> 0.259, cornell 1080p 0.180 -> 0.179 (17 KiB per workgroup; still 5 waves per SIMD)
+        __shared__ IndStash stash;
+        indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter, nullptr, nullptr, &stash);
     }
     if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
@@ -1407,6 +1442,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     if (zsplit ? blockIdx.z == 1u : (blockIdx.x & 1u) != 0u) {
         Scene sc = A.sc;
         if constexpr (LDS_I) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
+        // (no IndStash: its 17 KiB next to the direct role's park area cost the merged grid a wave per SIMD —
+        // cornell 4-way stripe 0.138 -> 0.159 ms, profiles/r05/c26)
         if (active) indirect_body<false>(A, sc, C2, x, y, n_top, n_emitter);
     } else if (active) {
         const Scene& sc = A.sc;
