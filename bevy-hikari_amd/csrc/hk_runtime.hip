@@ -67,7 +67,8 @@ struct OptDef {
     double def, lo, hi;
 };
 constexpr OptDef OPTS[OPT_COUNT] = {
-    {"pipeline_min_px", 1.2e6, 0.0, 1e12}, {"pipeline_heavy_min_px", 0.0, 0.0, 1e12}, {"gbuffer_pipeline", 1, 0, 1},  {"tail_pipeline", 1, 0, 1},
+    {"pipeline_min_px", 1.2e6, 0.0, 1e12}, {"pipeline_heavy_min_px", 0.0, 0.0, 1e12},
+    {"gbuffer_pipeline", 1, 0, 1},         {"tail_pipeline", 1, 0, 1},
     {"channel_streams", 1, 0, 1},          {"fuse", 1, 0, 1},              {"fuse_min_px", 1048576.0, 0.0, 1e12},
     {"merge", -1, -1, 1},                  {"bg_elision", 1, 0, 1},        {"spatial_view_planes", 1, 0, 1},
     {"band_full_windows", 0, 0, 1},        {"leaf_collapse", 1, 0, 1},     {"gbuffer_reuse", 1, 0, 1},
