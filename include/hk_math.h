@@ -82,13 +82,14 @@ HK_HD float hk_exp2(float x)
 
 HK_HD float hk_exp(float x) { return hk_exp2(x * 1.4426950408889634f); }
 
-/* hk_exp(x) without the selects of NaN and of x * log2(e) >= 128: the same bits for every x with x * log2(e) < 128
- * and a NaN (of another payload, possibly) for NaN.  For the denoiser's edge-stopping weights (denoise.wgsl:44-69:
- * exp of -|a| / b, b > 0), which are then clamped to [0, 1], where a NaN weight becomes 0 whatever its payload.
- * Checked against hk_exp on every input (hko_exp_weight_mismatches). */
+/* hk_exp(x) for the denoiser's edge-stopping weights (denoise.wgsl:44-69: exp of -|a| / b, b > 0, so x <= 0 or NaN),
+ * which are then clamped to [0, 1]: y clamped below at -160 (so a huge |x| or a NaN gives 0, which the clamp makes of
+ * a NaN weight anyway) and a one-step scale that flushes a weight below 2^-126 to 0 (WGSL leaves subnormal results
+ * to the implementation), without hk_exp's selects.  The same bits as hk_exp wherever that is a normal float;
+ * checked on every input x <= 0 (hko_exp_weight_mismatches). */
 HK_HD float hk_exp_weight(float x)
 {
-    const float y = x * 1.4426950408889634f;
+    const float y = hk_maxf(x * 1.4426950408889634f, -160.0f);
     float n = rintf(y);
     float f = y - n;
     float p = 1.5252733804059840e-05f;
@@ -99,12 +100,9 @@ HK_HD float hk_exp_weight(float x)
     p = HK_MAD(p, f, 2.4022650695910071e-01f);
     p = HK_MAD(p, f, 6.9314718055994531e-01f);
     p = HK_MAD(p, f, 1.0f);
-    const int32_t ni = (int32_t)hk_minf(hk_maxf(n, -160.0f), 160.0f);
-    const int normal = ni >= -126;
-    const float s1 = hk_u2f((uint32_t)(normal ? ni + 127 : ni + 64 + 127) << 23);
-    const float s2 = normal ? 1.0f : hk_u2f((uint32_t)(-64 + 127) << 23);
-    const float r = (p * s1) * s2;
-    return y < -151.0f ? 0.0f : r;
+    /* 2^n as an exponent field: 0 for n <= -127; for n >= -126 hk_exp's operations */
+    const int32_t ni = (int32_t)hk_maxf(n, -127.0f);
+    return p * hk_u2f((uint32_t)(ni + 127) << 23);
 }
 
 /* log2(x): x = m * 2^e with m in [sqrt(1/2), sqrt(2)); log2(m) via atanh series of s=(m-1)/(m+1).

@@ -2578,7 +2578,7 @@ static float log2_branchy(float x)
     float lm = (p * s) * 2.8853900817779268f;
     return (float)e + lm;
 }
-/* hk_exp_weight against hk_exp over every stride-th input with x * log2(e) < 128 (NaN: both NaN) */
+/* hk_exp_weight against hk_exp over every stride-th input x <= 0 (0 for NaN and where hk_exp is subnormal) */
 unsigned long long hko_exp_weight_mismatches(uint32_t stride)
 {
     unsigned long long bad = 0;
@@ -2586,9 +2586,11 @@ unsigned long long hko_exp_weight_mismatches(uint32_t stride)
 #pragma omp parallel for schedule(static) reduction(+ : bad)
     for (long long k = 0; k < n; ++k) {
         const float x = hk_u2f((uint32_t)(k * (long long)stride));
-        if (!(x * 1.4426950408889634f < 128.0f) && x == x) continue;
+        if (x > 0.0f) continue;  /* the weights' arguments: <= 0 or NaN */
         const float a = hk_exp_weight(x), b = hk_exp(x);
-        if (x != x ? a == a : hk_f2u(a) != hk_f2u(b)) ++bad;
+        /* equal bits, or 0 where hk_exp is below the normal range (flushed) */
+        const int ok = x != x ? a == 0.0f : (hk_f2u(a) == hk_f2u(b) || (a == 0.0f && b < 1.17549435e-38f));
+        if (!ok) ++bad;
     }
     return bad;
 }

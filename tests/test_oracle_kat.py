@@ -229,8 +229,9 @@ def test_branch_free_exp2_log2_equal_the_branchy_forms(oracle_lib):
 
 
 def test_exp_weight_equals_exp(oracle_lib):
-    """hk_exp_weight (the denoise levels' weights) gives hk_exp's bits wherever x * log2(e) < 128, NaN for NaN:
-    every 5th input here (all of them: 0 when run with stride 1)."""
+    """hk_exp_weight (the denoise levels' weights, arguments <= 0) gives hk_exp's bits wherever that is a normal
+    float, 0 where hk_exp is subnormal (flushed) and for NaN: every 5th input here (all of them: 0 when run with
+    stride 1)."""
     assert oracle_lib.hko_exp_weight_mismatches(5) == 0
 
 
