@@ -621,7 +621,8 @@ def main():
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world}" if stripes else
                                        f"cost-balanced row-bands x{world}") +
-                                      (" + RCCL per-peer exchange" if gather_mode == "peer" else " + RCCL all-gather")
+                                      ((" + gloo rehearsal on one GPU" if rehearsal else
+                                        " + RCCL per-peer exchange" if gather_mode == "peer" else " + RCCL all-gather"))
                                       if world > 1 else
                                       (f"single GPU through the RCCL path (world size 1, {gather_mode} gather)"
                                        if dist_on else "single GPU"),
