@@ -1442,9 +1442,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     if (zsplit ? blockIdx.z == 1u : (blockIdx.x & 1u) != 0u) {
         Scene sc = A.sc;
         if constexpr (LDS_I) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
-        // (no IndStash: its 17 KiB next to the direct role's park area cost the merged grid a wave per SIMD —
-        // cornell 4-way stripe 0.138 -> 0.159 ms, profiles/r05/c26)
-        if (active) indirect_body<false>(A, sc, C2, x, y, n_top, n_emitter);
+        // the IndStash in the launch's dynamic LDS after the staged scene, within the direct role's park area on
+        // validation frames (launch_light_merged sizes the buffer); a static one cost the merged grid a wave per SIMD
+        // (cornell 4-way stripe 0.138 -> 0.159 ms, profiles/r05/c26)
+        IndStash* stash = reinterpret_cast<IndStash*>(hk_lds_scene + (LDS_I ? stage_bytes(A.sc.bytes, PLAN_LIGHT) / 4u : 0u));
+        if (active) indirect_body<false>(A, sc, C2, x, y, n_top, n_emitter, nullptr, nullptr, stash);
     } else if (active) {
         const Scene& sc = A.sc;
         const DirectPixel P = load_direct_pixel(A, x, y);
@@ -2515,7 +2517,8 @@ void launch_light_merged(const FrameArgs& A, const ChannelArgs& C0, const Channe
     const bool vd = validation_frame(A.F.number, A.F.direct_validate_interval);
     const bool ve = validation_frame(A.F.number, A.F.emissive_validate_interval);
     const uint32_t park = (vd || ve) ? (uint32_t)(PARK_WORDS * 256 * sizeof(float)) : 0u;
-    const uint32_t lds = scene > park ? scene : park;
+    const uint32_t ind = scene + (uint32_t)sizeof(IndStash);  // the indirect role: staged scene + stash
+    const uint32_t lds = ind > park ? ind : park;
 #define HK_MERGED(VD_, VE_)                                                                                         \
     if (scene) hipLaunchKernelGGL((k_light_merged<VD_, VE_, true>), g, dim3(256), lds, st, A, C0, C1, C2);          \
     else hipLaunchKernelGGL((k_light_merged<VD_, VE_, false>), g, dim3(256), lds, st, A, C0, C1, C2);
