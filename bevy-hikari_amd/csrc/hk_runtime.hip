@@ -675,17 +675,22 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
 // For a static camera every other read is the pixel's own (temporal reprojection is the
 // identity), so the core rows stay bit-identical to the whole frame (test_gpu_row_bands_*),
 // with 1.15x instead of 1.30x the work of an 8-way city 4K band.  Rows outside a pass's window
-// keep stale values that no windowed pass reads; a settings change that widens a window (band_windows) zeroes
-// the rows it brings in and keeps the window wide from then on.  Option band_full_windows: every pass on all rows.
+// keep stale values that no windowed pass reads; a settings change that widens a window (band_windows) takes the
+// history of the rows it brings in from their owner bands (or zero-fills them) and keeps the window wide from
+// then on.  Option band_full_windows: every pass on all rows.
 constexpr int32_t DENOISE_OUT_REACH = 16, SPATIAL_RANGE = 20, EMISSIVE_SPATIAL_RANGE = 10;
 constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
 // Only for a static frame: under camera or instance motion temporal reprojection reads the previous
 // frame's reservoirs at other rows, so every pass runs on the whole band (velocity_zero is set by
 // hk_render_gbuffer before its own window is taken, and cleared by a host G-buffer plane upload).
+bool band_windowed(const hk_ctx* c)
+{
+    return !(c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows || !c->velocity_zero ||
+             c->on(OPT_BAND_FULL_WINDOWS));
+}
 FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
 {
-    if (c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows || !c->velocity_zero) return A;
-    if (c->on(OPT_BAND_FULL_WINDOWS)) return A;
+    if (!band_windowed(c)) return A;
     const int32_t lo = std::max(0, c->core_row0 - margin);
     const int32_t hi = std::min(c->s_rows, c->core_row0 + c->core_rows + margin);
     A.F.win_row0 = lo;
@@ -698,40 +703,80 @@ bool bg_elision_off(const hk_ctx* c) { return !c->on(OPT_BG_ELISION); }
 int32_t light_out_reach(const hk_settings* st) { return st->denoise ? DENOISE_OUT_REACH : 0; }
 // The settings-dependent margins of a band's light-pass windows (pass_window) as sticky maxima: a
 // setting turned on later (denoise, emissive or indirect spatial reuse) widens its channel's window, and the rows
-// it brings in hold reservoirs no pass has updated since the band was sized (or since a motion frame ran every
-// pass on the whole band).  Those rows' records of the channel's buffers are zeroed when the window first grows,
-// as hk_resize zero-fills them (light.rs:355-358), and the window then never narrows again, so every later toggle
-// of the setting is exact again.  The frame that widens the window differs from a whole-frame render near the
-// band's core edges (its new rows start without history): test_gpu_row_bands_settings_toggle.
-int band_windows(hk_ctx* c, const FrameArgs& A_all, const hk_settings* st, hipStream_t s)
+// it brings in hold records no pass of this band has updated since it was sized (or since a motion frame ran
+// every pass on the whole band).  A whole-frame render holds those rows' history — its temporal passes run on every
+// pixel whatever the spatial flags (light.rs:656-699) — and so does the band whose core the rows belong to (its
+// core rows equal the whole frame's).  window_growth lists the rows per reservoir buffer; the host copies them
+// from their owners between frames (hk_band_window_grow, hk_reservoir_rows: bands.refill_windows), and the frame
+// after that is bit-identical to a whole-frame render (test_gpu_row_bands_settings_toggle).  A window that grows
+// without the refill (hk_render_frame first) has its new rows zero-filled instead, as hk_resize zero-fills the
+// buffers (light.rs:355-358): exact again once the history has refilled.  The window never narrows.
+struct WindowGrowth {
+    int32_t want[3];                // the margins `st` needs: spatial pass (out), direct + emissive, indirect
+    int32_t rows[HK_RESERVOIR_BUFFERS][2][2];  // per buffer, above / below the core: local rows [r0, r1) to fill
+    bool grows, fill;               // some margin widens; its new rows need history (a windowed frame, not the first)
+};
+WindowGrowth window_growth(const hk_ctx* c, const hk_settings* st)
 {
+    WindowGrowth G{};
     const int32_t out = light_out_reach(st);
-    const int32_t want[3] = {out, out + (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0),
-                             out + (st->indirect_spatial_reuse ? SPATIAL_RANGE : 0)};
-    int32_t* have[3] = {&c->win_out, &c->win_emi, &c->win_ind};
+    G.want[0] = out;
+    G.want[1] = out + (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0);
+    G.want[2] = out + (st->indirect_spatial_reuse ? SPATIAL_RANGE : 0);
+    const int32_t have[3] = {c->win_out, c->win_emi, c->win_ind};
     // the buffers whose records the group's window holds: spatial pairs 4/5, 8/9; direct + emissive 0-5; indirect 6-9
-    static const int first[3][2] = {{4, 8}, {0, -1}, {6, -1}};
-    static const int count[3][2] = {{2, 2}, {6, 0}, {4, 0}};
-    const bool windowed = pass_window(c, A_all, 0).F.win_rows > 0;
+    static const uint32_t members[3] = {0x330u, 0x03Fu, 0x3C0u};
+    const bool windowed = band_windowed(c);
+    const int32_t core0 = c->core_row0, core1 = c->core_row0 + c->core_rows;
+    for (int b = 0; b < HK_RESERVOIR_BUFFERS; ++b) {
+        G.rows[b][0][0] = G.rows[b][1][0] = INT32_MAX;
+        G.rows[b][0][1] = G.rows[b][1][1] = INT32_MIN;
+    }
     for (int g = 0; g < 3; ++g) {
-        const int32_t old = *have[g], m = std::max(old, want[g]);
+        const int32_t old = have[g], m = std::max(old, G.want[g]);
         if (m == old) continue;
-        *have[g] = m;
+        G.grows = true;
         if (old < 0 || !windowed) continue;  // zero-filled since hk_resize, or every row computed this frame
-        const int32_t w = (int32_t)c->s[0], core0 = c->core_row0, core1 = c->core_row0 + c->core_rows;
+        G.fill = true;
         const int32_t span[2][2] = {{std::max(0, core0 - m), std::max(0, core0 - old)},
                                     {std::min(c->s_rows, core1 + old), std::min(c->s_rows, core1 + m)}};
-        for (int k = 0; k < 2; ++k)
-            for (int b = 0; b < count[g][k]; ++b)
-                for (int side = 0; side < 2; ++side) {
-                    const int32_t r0 = span[side][0], r1 = span[side][1];
-                    if (r1 <= r0) continue;
-                    for (uint32_t plane = 0; plane < 4; ++plane)
-                        HK_HIP(c, hipMemsetAsync(c->reservoirs[first[g][k] + b] + (size_t)plane * c->res_n + (size_t)r0 * w, 0,
-                                                 (size_t)(r1 - r0) * w * sizeof(uint4), s));
-                }
-        c->bg_valid[0] = c->bg_valid[1] = false;  // the elision masks no longer describe the buffers
+        for (int b = 0; b < HK_RESERVOIR_BUFFERS; ++b) {
+            if (!(members[g] >> b & 1u)) continue;
+            // union over the groups: the rows between two groups' spans lie in the narrower group's old window,
+            // which this band computed exactly, so they equal the owner's records as well
+            for (int side = 0; side < 2; ++side) {
+                if (span[side][1] <= span[side][0]) continue;
+                G.rows[b][side][0] = std::min(G.rows[b][side][0], span[side][0]);
+                G.rows[b][side][1] = std::max(G.rows[b][side][1], span[side][1]);
+            }
+        }
     }
+    for (int b = 0; b < HK_RESERVOIR_BUFFERS; ++b)
+        for (int side = 0; side < 2; ++side)
+            if (G.rows[b][side][1] <= G.rows[b][side][0]) G.rows[b][side][0] = G.rows[b][side][1] = 0;
+    return G;
+}
+void commit_growth(hk_ctx* c, const WindowGrowth& G)
+{
+    int32_t* have[3] = {&c->win_out, &c->win_emi, &c->win_ind};
+    for (int g = 0; g < 3; ++g) *have[g] = std::max(*have[g], G.want[g]);
+}
+int band_windows(hk_ctx* c, const hk_settings* st, hipStream_t s)
+{
+    const WindowGrowth G = window_growth(c, st);
+    if (!G.grows) return HK_OK;
+    commit_growth(c, G);
+    if (!G.fill) return HK_OK;
+    const size_t w = c->s[0];
+    for (int b = 0; b < HK_RESERVOIR_BUFFERS; ++b)
+        for (int side = 0; side < 2; ++side) {
+            const int32_t r0 = G.rows[b][side][0], r1 = G.rows[b][side][1];
+            if (r1 <= r0) continue;
+            for (uint32_t plane = 0; plane < 4; ++plane)
+                HK_HIP(c, hipMemsetAsync(c->reservoirs[b] + (size_t)plane * c->res_n + (size_t)r0 * w, 0,
+                                         (size_t)(r1 - r0) * w * sizeof(uint4), s));
+        }
+    c->bg_valid[0] = c->bg_valid[1] = false;  // the elision masks no longer describe the buffers
     return HK_OK;
 }
 
@@ -1609,6 +1654,10 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     if (!settings || !in) return fail(c, HK_ERR_INVALID, "null settings or frame inputs");
     float want = settings->upscale_ratio < 1.0f ? 1.0f : (settings->upscale_ratio > 2.0f ? 2.0f : settings->upscale_ratio);
     if (want != c->ratio) return fail(c, HK_ERR_STATE, "settings.upscale_ratio differs from the hk_resize ratio");
+    // every argument / state check before any scheduling state changes: a rejected call leaves the
+    // next frame's pipelining as it was
+    if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
+        return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     (void)hipSetDevice(c->device);
     hipStream_t st = pick_frame(c, stream);
     c->heavy = settings->indirect_spatial_reuse || settings->emissive_spatial_reuse || c->dn_calls > 0;  // pipeline_size
@@ -1650,8 +1699,6 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     }
     c->rf_swapped = swap;
     c->tail_open = false;
-    if (c->stripe_n >= 2 && (settings->emissive_spatial_reuse || settings->indirect_spatial_reuse))
-        return fail(c, HK_ERR_STATE, "interleaved stripes (hk_resize_striped) exclude spatial reuse: it reads neighbours");
     c->head = in->frame_number & 1u;
     c->timing_frame = in->frame_number % c->timing_every == 0u;
     FrameArgs A = frame_args(c, settings, in);
@@ -1675,7 +1722,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // pass reads (core +-(OUT + that channel's range): direct_lit has no spatial pass, light.rs:656-676),
     // then spatial reuse.  A: the indirect channel; AE: direct + emissive.
     // (sticky margins: band_windows)
-    HK_TRY(band_windows(c, A_all, settings, st));
+    HK_TRY(band_windows(c, settings, st));
     A = pass_window(c, A_all, c->win_ind);
     FrameArgs AE = pass_window(c, A_all, c->win_emi);
     const FrameArgs AS = pass_window(c, A_all, c->win_out);
@@ -2164,6 +2211,53 @@ int hk_load_reservoirs(hk_ctx* c, int id, const hk_packed_reservoir* src, size_t
     }
     HK_HIP(c, hipMemcpyAsync(c->reservoirs[id], planes.data(), planes.size() * sizeof(uint4), hipMemcpyHostToDevice, st));
     c->bg_valid[0] = c->bg_valid[1] = false;  // the elision masks no longer describe the buffers
+    HK_HIP(c, hipStreamSynchronize(st));
+    return HK_OK;
+}
+
+int hk_band_window_grow(hk_ctx* c, const hk_settings* settings, int32_t* ranges, int commit)
+{
+    if (!c || !settings || !ranges) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    const WindowGrowth G = window_growth(c, settings);
+    int n = 0;
+    for (int b = 0; b < HK_RESERVOIR_BUFFERS; ++b) {
+        bool any = false;
+        for (int side = 0; side < 2; ++side) {
+            const int32_t r0 = G.rows[b][side][0], r1 = G.rows[b][side][1];
+            ranges[4 * b + 2 * side] = r1 > r0 ? c->s_row0 + r0 : 0;
+            ranges[4 * b + 2 * side + 1] = r1 > r0 ? r1 - r0 : 0;
+            any |= r1 > r0;
+        }
+        n += any;
+    }
+    if (commit && G.grows) commit_growth(c, G);
+    return n;
+}
+
+int hk_reservoir_rows(hk_ctx* c, int id, int32_t frame_row0, int32_t rows, void* data, int store, void* stream)
+{
+    if (!c || !data || id < 0 || id >= HK_RESERVOIR_BUFFERS || rows < 0) return HK_ERR_INVALID;
+    if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
+    if (c->stripe_n >= 2) return fail(c, HK_ERR_STATE, "hk_reservoir_rows needs a contiguous band (not stripes)");
+    const int32_t r0 = frame_row0 - c->s_row0;
+    if (r0 < 0 || r0 + rows > c->s_rows) return fail(c, HK_ERR_INVALID, "rows outside the context's band");
+    if (rows == 0) return HK_OK;
+    (void)hipSetDevice(c->device);
+    hipStream_t st = pick(c, stream);
+    HK_TRY(gb_join(c, st));
+    // after every pass the frame sequence enqueued (its side streams joined its stream before returning)
+    if (c->frame_st && c->frame_st != st) {
+        HK_HIP(c, hipEventRecord(c->ev_frame_mark, c->frame_st));
+        HK_HIP(c, hipStreamWaitEvent(st, c->ev_frame_mark, 0));
+    }
+    const size_t w = c->s[0], n = (size_t)rows * w;
+    for (size_t k = 0; k < 4; ++k) {
+        uint4* dev = c->reservoirs[id] + k * c->res_n + (size_t)r0 * w;
+        uint4* ext = reinterpret_cast<uint4*>(data) + k * n;
+        HK_HIP(c, hipMemcpyAsync(store ? dev : ext, store ? ext : dev, n * sizeof(uint4), hipMemcpyDefault, st));
+    }
+    if (store) c->bg_valid[0] = c->bg_valid[1] = false;  // the elision masks no longer describe the buffers
     HK_HIP(c, hipStreamSynchronize(st));
     return HK_OK;
 }

@@ -188,3 +188,81 @@ def peer_gather(full, mine, rank: int, world: int) -> list:
         ops.append(dist.P2POp(dist.isend, mine, dst))
         ops.append(dist.P2POp(dist.irecv, full[src * n: (src + 1) * n], src))
     return dist.batch_isend_irecv(ops) if ops else []
+
+
+# ---------------------------------------------------------------- band window refill (settings changes)
+# A band runs each channel's light passes on its core rows +- the margin the settings need; turning a setting on
+# (denoise, emissive / indirect spatial reuse) widens a margin for good, and the rows it takes in hold records the
+# band never computed, where a whole-frame render holds their history (its temporal passes run on every pixel,
+# light.rs:656-699).  The band owning those rows as core rows holds them exactly, so before the first frame with the
+# new settings every band takes them from their owners (hk_band_window_grow lists them, hk_reservoir_rows moves
+# them) and commits the wider windows: the frame stays bit-identical to the whole-frame render.  Call it on frames
+# whose settings differ from the previous frame's (a no-op otherwise), after hk_render_gbuffer, before
+# hk_render_frame.
+def _overlap(y0: int, n: int, lo: int, hi: int):
+    a, b = max(y0, lo), min(y0 + n, hi)
+    return (a, b - a) if b > a else None
+
+
+def refill_windows_local(bands, settings) -> int:
+    """In-process refill over the bands of one frame (one context per band, e.g. on one GPU): `bands` is a list of
+    (Band, renderer).  Returns the number of row blocks copied."""
+    needs = [r.band_window_grow(settings) for _, r in bands]
+    moved = 0
+    for (_, r), ranges in zip(bands, needs):
+        for buf in range(len(ranges)):
+            for side in range(2):
+                y0, n = int(ranges[buf, 2 * side]), int(ranges[buf, 2 * side + 1])
+                for ob, owner in bands:
+                    if owner is r:
+                        continue
+                    o = _overlap(y0, n, ob.y0, ob.y0 + ob.rows)
+                    if o:
+                        r.reservoir_rows(buf, o[0], o[1], owner.reservoir_rows(buf, o[0], o[1]), store=True)
+                        moved += 1
+    for _, r in bands:
+        r.band_window_grow(settings, commit=True)
+    return moved
+
+
+def refill_windows(renderer, settings, bounds, rank: int, world: int, device="cuda") -> int:
+    """The refill across ranks (one band per rank, bands = `bounds`): every rank's needs all-gathered, each block
+    sent by its owner straight to the rank that needs it (batch_isend_irecv: RCCL over xGMI on GPUs, gloo with
+    device "cpu").  Collective: every rank calls it.  Returns the number of row blocks this rank received."""
+    import torch
+    import torch.distributed as dist
+    mine = renderer.band_window_grow(settings)
+    t = torch.from_numpy(np.ascontiguousarray(mine.reshape(-1))).to(device)
+    everyone = torch.zeros(world * t.numel(), dtype=t.dtype, device=device)
+    dist.all_gather_into_tensor(everyone, t)
+    need = everyone.cpu().numpy().reshape(world, *mine.shape)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    ops, stores = [], []
+    # one pass per (sender, receiver) pair in the same (buffer, side) order on both ends, so point-to-point
+    # messages between two ranks match in posting order
+    for q in range(world):
+        for buf in range(need.shape[1]):
+            for side in range(2):
+                y0, n = int(need[q, buf, 2 * side]), int(need[q, buf, 2 * side + 1])
+                if q == rank:
+                    for p in range(world):
+                        o = _overlap(y0, n, int(bounds[p]), int(bounds[p + 1])) if p != rank else None
+                        if o:
+                            block = torch.empty(renderer.reservoir_rows_bytes(o[1]), dtype=torch.uint8, device=device)
+                            ops.append(dist.P2POp(dist.irecv, block, p))
+                            stores.append((buf, o, block))
+                else:
+                    o = _overlap(y0, n, lo, hi)
+                    if o:
+                        block = torch.empty(renderer.reservoir_rows_bytes(o[1]), dtype=torch.uint8, device=device)
+                        renderer.reservoir_rows(buf, o[0], o[1], block.data_ptr() if block.is_cuda else block.numpy())
+                        ops.append(dist.P2POp(dist.isend, block, q))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        if str(device).startswith("cuda"):
+            torch.cuda.synchronize()
+    for buf, o, block in stores:
+        renderer.reservoir_rows(buf, o[0], o[1], block.data_ptr() if block.is_cuda else block.numpy(), store=True)
+    renderer.band_window_grow(settings, commit=True)
+    return len(stores)

@@ -125,6 +125,35 @@ class HikariRenderer:
         _check(self.ctx, self._L.hk_band_info(self.ctx, *[C.byref(x) for x in v]), "hk_band_info")
         return tuple(x.value for x in v)
 
+    def band_window_grow(self, settings: _abi.hk_settings, commit: bool = False) -> np.ndarray:
+        """(10, 4) int32: per reservoir buffer the (frame row, rows) above and below the band's core whose records
+        the next hk_render_frame with `settings` needs from their owner bands (hk_band_window_grow); commit widens
+        the band's windows without zero-filling (after the rows were loaded)."""
+        ranges = np.zeros((_abi.RESERVOIR_BUFFERS, 4), np.int32)
+        rc = self._L.hk_band_window_grow(self.ctx, C.byref(settings), ranges.ctypes.data, int(commit))
+        _check(self.ctx, min(rc, 0), "hk_band_window_grow")
+        return ranges
+
+    def reservoir_rows_bytes(self, rows: int) -> int:
+        return 4 * rows * self.width * 16
+
+    def reservoir_rows(self, buffer_id: int, frame_row0: int, rows: int, data=None, store: bool = False,
+                       stream=None):
+        """Records of frame rows [frame_row0, frame_row0 + rows) of a reservoir buffer in the row-exchange layout
+        (hk_reservoir_rows): store False copies them out (into `data`: a uint8 array, or a device address; a new
+        array when None, returned), store True copies `data` in."""
+        if data is None:
+            data = np.empty(self.reservoir_rows_bytes(rows), np.uint8)
+        if isinstance(data, np.ndarray):
+            if not data.flags.c_contiguous or data.nbytes != self.reservoir_rows_bytes(rows):
+                raise ValueError("reservoir row data must be a contiguous array of reservoir_rows_bytes(rows) bytes")
+            ptr = data.ctypes.data
+        else:
+            ptr = int(data)
+        _check(self.ctx, self._L.hk_reservoir_rows(self.ctx, buffer_id, frame_row0, rows, ptr, int(store),
+                                                   _stream(stream)), "hk_reservoir_rows")
+        return data
+
     # ---- per frame
     def render_gbuffer(self, inputs: _abi.hk_frame_inputs, stream=None) -> None:
         _check(self.ctx, self._L.hk_render_gbuffer(self.ctx, C.byref(inputs), _stream(stream)), "hk_render_gbuffer")

@@ -124,6 +124,19 @@ class Camera:
     near: float = 0.1
 
     def view(self, width: int, height: int) -> _abi.hk_view:
+        # the view of an unchanged camera is computed once (the per-frame host work of a static camera is then
+        # a struct copy: ~80 -> ~10 us per frame_inputs)
+        key = (width, height, self.fov_y, self.near, tuple(np.asarray(self.transform.translation, np.float64)),
+               tuple(np.asarray(self.transform.rotation, np.float64)), tuple(np.asarray(self.transform.scale, np.float64)))
+        cache = self.__dict__.setdefault("_view_cache", {})
+        hit = cache.get(key)
+        if hit is None:
+            if len(cache) > 64:
+                cache.clear()
+            hit = cache[key] = self._view(width, height)
+        return _abi.hk_view.from_buffer_copy(hit)
+
+    def _view(self, width: int, height: int) -> _abi.hk_view:
         proj = perspective_infinite_reverse_rh(self.fov_y, width / height, self.near)
         world = self.transform.matrix()
         view_proj = proj @ np.linalg.inv(world)

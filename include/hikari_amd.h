@@ -294,6 +294,24 @@ int hk_set_band_halo(hk_ctx* ctx, uint32_t rows);
 /* band geometry after hk_resize: local rows [0, rows) hold global rows [row0, row0+rows);
  * the band's own (non-halo) rows are local [core_row0, core_row0+core_rows) */
 int hk_band_info(const hk_ctx* ctx, int32_t* row0, int32_t* rows, int32_t* core_row0, int32_t* core_rows);
+/* Band window refill (no reference counterpart: the reference renders one whole frame, whose temporal passes run
+ * on every pixel whatever the spatial flags, light.rs:656-699).  A band runs each channel's light passes on its
+ * core rows +- the margin `settings` needs (that channel's spatial range plus the denoiser's reach); a setting turned
+ * on later widens the margin for good, and the rows it takes in hold records this band never computed.  Their
+ * owner (the band whose core rows they are) holds them exactly.  For the next hk_render_frame with `settings`,
+ * ranges[4 k + 0..3] = (frame row, rows) above the core and (frame row, rows) below it of reservoir buffer k's
+ * records to take from the owners (rows 0 = none), k = 0..HK_RESERVOIR_BUFFERS-1; returns how many buffers need
+ * any (< 0: error).  commit != 0 then widens the margins as hk_render_frame would, without zero-filling: call it
+ * after loading the rows (hk_reservoir_rows).  Without a committed refill hk_render_frame zero-fills the new rows
+ * (as hk_resize does, light.rs:355-358).  Call between frames: after the last frame's hk_render_frame (and this
+ * frame's hk_render_gbuffer), on every band of the frame. */
+int hk_band_window_grow(hk_ctx* ctx, const hk_settings* settings, int32_t* ranges, int commit);
+/* The records of frame rows [frame_row0, frame_row0 + rows) of reservoir buffer `id`, which must lie in this
+ * context's band: out of the context (store = 0) into `data`, or from `data` into it (store = 1).  `data` is host
+ * memory or a device pointer of any device of the process, in the row-exchange layout: 4 x rows x width chunks of
+ * 16 bytes (the context's four record chunks, each a plane of rows x width), the layout the same call of another
+ * band's context reads and writes.  Ordered after the frame work queued so far; blocking. */
+int hk_reservoir_rows(hk_ctx* ctx, int id, int32_t frame_row0, int32_t rows, void* data, int store, void* stream);
 
 /* ---- per frame ---- */
 /* Primary-ray G-buffer (prepass.wgsl:84-100).  Pixel (x, y) traces the ray through

@@ -342,25 +342,28 @@ def test_gpu_row_bands_match_whole_frame(spatial, denoise, world, H):
     assert total == o.counters()
 
 
-def test_gpu_row_bands_settings_toggle():
+@pytest.mark.parametrize("refill", [True, False], ids=["refill", "zero_fill"])
+def test_gpu_row_bands_settings_toggle(refill):
     """A band's light-pass windows depend on the settings (hk_runtime.hip pass_window: each channel's temporal pass on
-    core +-(OUT + its spatial range)); turning emissive spatial reuse on at frame 4 widens the direct / emissive
-    window, and the rows it brings in have no reservoir history.  band_windows zeroes them and keeps the window
-    wide from then on.  Before the toggle every band's core rows equal the whole-frame render bit for
-    bit.  While emissive spatial reuse is on, it reads the new rows' emissive records, whose history started at the
-    toggle, so the core rows near the bands' edges differ: measured 93-98 % of pixels exact, mean relative difference
-    <= 1.5e-4 (profiles/r05/c9), held here to >= 90 % and <= 2e-3.  With the setting off again (frame 7) nothing reads
-    those rows and the core rows are bit-exact again; turning it on once more (frames 8-9) changes no window."""
+    core +-(OUT + its spatial range)); turning the denoiser on at frame 4 widens every window, emissive spatial reuse
+    at frame 6 the direct / emissive one.  The rows a window takes in hold no history of this band; their owner bands
+    hold it exactly, and bands.refill_windows_local copies it over (hk_band_window_grow + hk_reservoir_rows) before the
+    frame: every band's core rows equal the whole-frame render bit for bit on every frame.
+    Without the refill (zero_fill) hk_render_frame zero-fills the new rows (hk_resize's state): exact before the first
+    widening; afterwards the new rows' ReSTIR chains restart and the denoiser spreads the difference over the core rows
+    (measured 47-78 % of pixels exact, mean relative difference <= 5.5e-3: profiles/r06/c2), held to <= 1e-2."""
     from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
-    from hikari_amd.bands import band_of, halo_rows
+    from hikari_amd.bands import band_of, halo_rows, refill_windows_local
     from oracle import Oracle
     W, H, world = 64, 192, 3
     scene, cam, lights = examples.cornell()
     desc = scene.build()
-    on = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, emissive_spatial_reuse=True,
-                        denoise=True).to_c()
-    off = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, emissive_spatial_reuse=False,
-                         denoise=True).to_c()
+
+    def settings(emissive, denoise):
+        return HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True,
+                              emissive_spatial_reuse=emissive, denoise=denoise).to_c()
+    # (emissive spatial reuse, denoise) per frame: denoise on at 4, emissive spatial reuse on at 6, off at 8, on at 9
+    plan = [(False, False)] * 4 + [(False, True)] * 2 + [(True, True)] * 2 + [(False, True), (True, True), (True, True)]
     o = Oracle(desc, load_noise(), W, H, 1.0)
     ranks = []
     for k in range(world):
@@ -371,15 +374,24 @@ def test_gpu_row_bands_settings_toggle():
         r.set_band_halo(halo_rows(True, True))
         r.resize(W, H, 1.0, b.y0, b.rows)
         ranks.append((b, r))
-    errors, worst = [], []
-    for f in range(10):
-        s = on if 4 <= f < 7 or f >= 8 else off
+    errors, worst, moved = [], [], []
+    previous = None
+    for f, (emissive, denoise) in enumerate(plan):
+        s = settings(emissive, denoise)
         fi = frame_inputs(f, cam, lights, W, H)
-        for x in [o] + [r for _, r in ranks]:
-            x.render_gbuffer(fi)
-            x.render_frame(s, fi)
-            x.denoise(s, fi)
-            x.tone_sum(s)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.denoise(s, fi)
+        o.tone_sum(s)
+        for _, r in ranks:
+            r.render_gbuffer(fi)
+        if refill and (emissive, denoise) != previous:
+            moved.append((f, refill_windows_local(ranks, s)))
+        previous = (emissive, denoise)
+        for _, r in ranks:
+            r.render_frame(s, fi)
+            r.denoise(s, fi)
+            r.tone_sum(s)
         whole = canon_plane(10, o.output(10)).reshape(H, W, 4)
         for b, r in ranks:
             row0, rows, core0, core_rows = r.band_info()
@@ -390,11 +402,15 @@ def test_gpu_row_bands_settings_toggle():
             fc = c.view(np.float16).astype(np.float32)[..., :3]
             rel = float(np.abs(fa - fc).sum() / max(np.abs(fc).sum(), 1e-6))
             worst.append((f, b.y0, round(exact, 4), round(rel, 5)))
-            if (f < 4 or f == 7) and exact < 1.0:
-                errors.append(f"frame {f} band {b.y0}: {exact:.4f} of pixels exact with emissive spatial reuse off")
-            if exact < 0.90 or rel > 0.002:
+            if (refill or f < 4) and exact < 1.0:
+                errors.append(f"frame {f} band {b.y0}: {exact:.4f} of pixels exact")
+            if not np.isfinite(fa).all() or rel > 0.01:
                 errors.append(f"frame {f} band {b.y0}: {exact:.4f} of pixels exact, mean relative difference {rel:.4f}")
     assert not errors, "\n".join(errors) + f"\n{worst}"
+    if refill:
+        # the widening frames moved rows (both inner bands on both sides, the outer bands on one side)
+        grown = dict(moved)
+        assert grown[0] == 0 and grown[4] > 0 and grown[6] > 0 and grown[8] == 0 and grown[9] == 0, moved
 
 
 def test_gpu_row_bands_moving_camera_within_tolerance():

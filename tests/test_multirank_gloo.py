@@ -371,3 +371,118 @@ def test_reassembly_row_copies_equal_the_gather_index(world, height):
             dst.copy_(src)
         assert torch.equal(out, frame)
         assert torch.equal(gathered[torch.from_numpy(index)], frame)
+
+
+class _FakeBand:
+    """Stands in for a band context in the window refill's exchange logic (bands.refill_windows): reservoir buffers
+    as (4, rows, W, 16) byte planes in the row-exchange layout of hk_reservoir_rows; the core rows hold the
+    whole frame's records (a pattern of buffer, frame row and column), the halo rows garbage until refilled.  Its
+    needs are what hk_band_window_grow lists for windows widening from 0 to `margins[buffer]` rows."""
+    HALO = 40  # bands.DEFAULT_HALO
+
+    def __init__(self, band, height, width, margins):
+        self.band, self.width = band, width
+        self.row0 = max(0, band.y0 - self.HALO)
+        self.rows = min(height, band.y0 + band.rows + self.HALO) - self.row0
+        rng = np.random.default_rng(band.y0)
+        self.store = rng.integers(0, 256, (len(margins), 4, self.rows, width, 16), dtype=np.uint8)
+        for b in range(len(margins)):
+            for y in range(band.y0, band.y0 + band.rows):
+                self.store[b, :, y - self.row0] = self.truth(b, y, width)
+        self.ranges = np.zeros((len(margins), 4), np.int32)
+        for b, m in enumerate(margins):
+            lo, hi = band.y0, band.y0 + band.rows
+            a0, a1 = max(0, lo - m), lo
+            b0, b1 = hi, min(height, hi + m)
+            self.ranges[b] = [a0 if a1 > a0 else 0, a1 - a0, b0 if b1 > b0 else 0, max(0, b1 - b0)]
+        self.committed = False
+
+    @staticmethod
+    def truth(buf, y, width):
+        x = np.arange(width)
+        v = (buf * 131 + y * 7 + x[:, None] * 3 + np.arange(16)[None, :]) % 251
+        return np.broadcast_to(v.astype(np.uint8), (4, width, 16))
+
+    def band_window_grow(self, settings, commit=False):
+        if commit:
+            self.committed = True
+        return self.ranges.copy()
+
+    def reservoir_rows_bytes(self, rows):
+        return 4 * rows * self.width * 16
+
+    def reservoir_rows(self, buf, frame_row0, rows, data=None, store=False, stream=None):
+        r0 = frame_row0 - self.row0
+        assert 0 <= r0 and r0 + rows <= self.rows
+        if data is None:
+            data = np.empty(self.reservoir_rows_bytes(rows), np.uint8)
+        view = data.reshape(4, rows, self.width, 16)
+        if store:
+            self.store[buf, :, r0: r0 + rows] = view
+        else:
+            view[...] = self.store[buf, :, r0: r0 + rows]
+        return data
+
+    def check(self):
+        for b in range(len(self.ranges)):
+            for side in range(2):
+                y0, n = self.ranges[b, 2 * side], self.ranges[b, 2 * side + 1]
+                for y in range(y0, y0 + n):
+                    assert np.array_equal(self.store[b, :, y - self.row0], self.truth(b, y, self.width)), (b, y)
+        assert self.committed
+
+
+MARGINS = [0, 10, 10, 10, 16, 16, 20, 20, 36, 36]
+
+
+def _refill_worker(rank, world, port, bounds, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root / "bevy-hikari_amd"))
+    import torch.distributed as dist
+
+    from hikari_amd.bands import band_of, refill_windows
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = -1
+    try:
+        fake = _FakeBand(band_of(rank, world, bounds[-1], bounds), bounds[-1], 8, MARGINS)
+        got = refill_windows(fake, None, bounds, rank, world, device="cpu")
+        fake.check()
+        q.put((rank, got, None))
+    except Exception as e:  # reported through the queue, so the test fails instead of waiting
+        q.put((rank, got, repr(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bounds", [[0, 48, 96], [0, 40, 56, 120, 160], [0, 24, 48, 72, 96, 120, 144]],
+                         ids=["world2", "world4-uneven", "world6-narrow"])
+def test_band_window_refill_exchange(bounds):
+    """bands.refill_windows (a settings change widening the bands' light-pass windows): every rank's needs are
+    all-gathered and each row block comes point-to-point from the band whose core holds it — across two bands when
+    a band is narrower than the margin (world6-narrow: 24-row bands, 36-row margins); the in-process form
+    (refill_windows_local) moves the same blocks."""
+    import torch.multiprocessing as mp
+
+    from hikari_amd.bands import band_of, refill_windows_local
+    world = len(bounds) - 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_refill_worker, args=(r, world, port, bounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(err is None for _, _, err in res), res
+    local = [(band_of(k, world, bounds[-1], bounds), _FakeBand(band_of(k, world, bounds[-1], bounds), bounds[-1], 8,
+                                                               MARGINS)) for k in range(world)]
+    moved = refill_windows_local(local, None)
+    for _, fake in local:
+        fake.check()
+    assert moved == sum(got for _, got, _ in res) > 0
