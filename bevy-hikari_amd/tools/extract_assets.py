@@ -15,24 +15,26 @@ import sys
 from pathlib import Path
 
 import numpy as np
-from PIL import Image
 
-REF = Path(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+REF = Path(sys.argv[1] if len(sys.argv) > 1 and __name__ == "__main__" else "/root/reference")
 OUT = Path(__file__).resolve().parent.parent / "hikari_amd" / "assets"
 
 
-def main():
-    OUT.mkdir(parents=True, exist_ok=True)
+def blue_noise(ref: Path) -> np.ndarray:
+    """The 16 noise textures decoded: (16, 64, 64, 4) uint8, texture-major."""
+    from PIL import Image
     tex = []
     for i in range(16):
-        im = Image.open(REF / "src" / "noise" / f"LDR_RGBA_{i}.png")
+        im = Image.open(ref / "src" / "noise" / f"LDR_RGBA_{i}.png")
         a = np.asarray(im.convert("RGBA"), dtype=np.uint8)
         assert a.shape == (64, 64, 4), a.shape
         tex.append(a)
-    np.stack(tex).tofile(OUT / "blue_noise_16x64x64_rgba8.bin")
-    shutil.copyfile(REF / "assets" / "models" / "cornell.glb", OUT / "cornell.glb")
+    return np.stack(tex)
 
-    g = json.loads((REF / "assets" / "models" / "City" / "scene.gltf").read_text())
+
+def city_layout(ref: Path) -> dict:
+    """The City proxy's layout from assets/models/City/scene.gltf."""
+    g = json.loads((ref / "assets" / "models" / "City" / "scene.gltf").read_text())
     layout = {"source": "assets/models/City/scene.gltf (JSON only; scene.bin missing)",
               "scene_roots": g["scenes"][g.get("scene", 0)]["nodes"], "nodes": [], "meshes": [], "materials": []}
     for n in g["nodes"]:
@@ -54,7 +56,18 @@ def main():
             "name": mat.get("name"), "base_color": pbr.get("baseColorFactor", [1, 1, 1, 1]),
             "metallic": pbr.get("metallicFactor", 1.0), "roughness": pbr.get("roughnessFactor", 1.0),
             "emissive": mat.get("emissiveFactor", [0, 0, 0])})
-    (OUT / "city_layout.json").write_text(json.dumps(layout, separators=(",", ":")))
+    return layout
+
+
+def city_layout_text(layout: dict) -> str:
+    return json.dumps(layout, separators=(",", ":"))
+
+
+def main():
+    OUT.mkdir(parents=True, exist_ok=True)
+    blue_noise(REF).tofile(OUT / "blue_noise_16x64x64_rgba8.bin")
+    shutil.copyfile(REF / "assets" / "models" / "cornell.glb", OUT / "cornell.glb")
+    (OUT / "city_layout.json").write_text(city_layout_text(city_layout(REF)))
 
 
 if __name__ == "__main__":
