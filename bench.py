@@ -360,6 +360,10 @@ def main():
     full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
         if dist_on and not peer else None
     peer_t = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] if peer else None
+    # world size 1: the per-peer exchange sends the band to this rank itself (bands.peer_exchange self_buf), so the
+    # line carries the RCCL point-to-point group's launch, transfer and device-side wait of every frame
+    self_t = [torch.empty((core_rows, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
+        if peer and world == 1 and not rehearsal else None
     pending = [None, None]
     if reorder:  # stripes / uneven bands back in frame order, on a side stream after each gather
         frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
@@ -450,7 +454,7 @@ def main():
                     wait_all(peer_exchange(host, bounds, rank, world))
                     peer_t[k].copy_(host)
                 else:
-                    pending[k] = peer_exchange(peer_t[k], bounds, rank, world)
+                    pending[k] = peer_exchange(peer_t[k], bounds, rank, world, None if self_t is None else self_t[k])
             return
         with torch.cuda.stream(comm):
             if pending[k] is not None:
@@ -470,7 +474,7 @@ def main():
                     dist.all_gather(parts, band_t[k].cpu())
                     full_t[k].copy_(torch.cat(parts))
             elif peer_stripes:
-                pending[k] = peer_gather(full_t[k], band_t[k], rank, world)
+                pending[k] = peer_gather(full_t[k], band_t[k], rank, world, self_transfer=world == 1)
             else:
                 pending[k] = dist.all_gather_into_tensor(full_t[k], band_t[k], async_op=True)
         if reorder and comm_mode != "noreorder":
@@ -624,7 +628,10 @@ def main():
                                       ((" + gloo rehearsal on one GPU" if rehearsal else
                                         " + RCCL per-peer exchange" if gather_mode == "peer" else " + RCCL all-gather"))
                                       if world > 1 else
-                                      (f"single GPU through the RCCL path (world size 1, {gather_mode} gather)"
+                                      (f"single GPU through the RCCL path (world size 1, " +
+                                       ("per-peer exchange as an RCCL self send/recv of the frame)"
+                                        if peer or peer_stripes else
+                                        f"{gather_mode} gather)")
                                        if dist_on else "single GPU"),
                        "band_bounds": None if bounds is None else [int(v) for v in bounds],
                        "band_calibration": balance or None},

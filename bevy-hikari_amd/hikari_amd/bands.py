@@ -167,20 +167,31 @@ def peer_exchange_ops(frame, bounds, rank: int, world: int) -> list:
     return ops
 
 
-def peer_exchange(frame, bounds, rank: int, world: int) -> list:
-    """Start the per-peer gather; returns the requests (wait() each)."""
+def peer_exchange(frame, bounds, rank: int, world: int, self_buf=None) -> list:
+    """Start the per-peer gather; returns the requests (wait() each).  self_buf (world size 1 only): the band is also
+    sent to this rank itself and received into self_buf (a tensor of the band's shape), so that a one-rank run
+    issues the per-peer path's RCCL point-to-point group — one send and one receive of a band, the transfer every
+    link carries at N > 1 — instead of no collective work at all."""
     import torch.distributed as dist
     ops = peer_exchange_ops(frame, bounds, rank, world)
+    if world == 1 and self_buf is not None:
+        mine = frame[bounds[rank]: bounds[rank + 1]]
+        ops = [dist.P2POp(dist.isend, mine, rank), dist.P2POp(dist.irecv, self_buf, rank)]
     return dist.batch_isend_irecv(ops) if ops else []
 
 
-def peer_gather(full, mine, rank: int, world: int) -> list:
+def peer_gather(full, mine, rank: int, world: int, self_transfer: bool = False) -> list:
     """The per-peer form of all_gather_into_tensor(full, mine) for the interleaved stripes' padded rows (or any
     equal-size parts): `mine` sent to every peer, peer j's part received into full[j * n : (j + 1) * n] (n =
     len(mine)), this rank's own part copied into its slot; returns the requests (wait() each).  The slots keep the
-    all-gather's layout, so bench.py's reassembly (reassembly_copies / stripe_gather_rows) applies unchanged."""
+    all-gather's layout, so bench.py's reassembly (reassembly_copies / stripe_gather_rows) applies unchanged.
+    self_transfer (world size 1 only): this rank's own part reaches its slot by an RCCL send to itself instead of a
+    copy, so a one-rank run issues the per-peer path's point-to-point group."""
     import torch.distributed as dist
     n = mine.shape[0]
+    if world == 1 and self_transfer:
+        return dist.batch_isend_irecv([dist.P2POp(dist.isend, mine, rank),
+                                       dist.P2POp(dist.irecv, full[rank * n: (rank + 1) * n], rank)])
     full[rank * n: (rank + 1) * n].copy_(mine)
     ops = []
     for k in range(1, world):

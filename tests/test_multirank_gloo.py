@@ -486,3 +486,4 @@ def test_band_window_refill_exchange(bounds):
     for _, fake in local:
         fake.check()
     assert moved == sum(got for _, got, _ in res) > 0
+
