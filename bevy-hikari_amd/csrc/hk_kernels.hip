@@ -21,6 +21,24 @@
 
 namespace hk {
 
+#ifdef HK_LANE_STATS
+__device__ unsigned long long hk_lane_stats_dev[2];
+#endif
+// traverse_top lane statistics since the last call (builds with -DHK_LANE_STATS; false otherwise)
+bool lane_stats_take(unsigned long long out[2], hipStream_t st)
+{
+#ifdef HK_LANE_STATS
+    unsigned long long zero[2] = {0, 0};
+    if (hipStreamSynchronize(st) != hipSuccess) return false;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hk_lane_stats_dev), sizeof(zero)) != hipSuccess) return false;
+    return hipMemcpyToSymbol(HIP_SYMBOL(hk_lane_stats_dev), zero, sizeof(zero)) == hipSuccess;
+#else
+    (void)st;
+    out[0] = out[1] = 0;
+    return false;
+#endif
+}
+
 // workgroup -> 16x16 tile -> pixel (global coordinates).  Tile orders:
 // RASTER: blockIdx in raster order; workgroups are dealt round-robin over the 8 XCDs, so every
 //   XCD works on the same band of the frame at once and per-region cost differences (sky vs.
@@ -1362,7 +1380,7 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
 }
 
 // ------------------------------------------------------------------ persistent waves (the north star's layout)
-// HK_PERSIST=1: a light pass as persistent waves instead of one workgroup per 16x16 tile.  The grid is what
+// Option persistent_indirect = 1 (hk_set_option): a light pass as persistent waves instead of one workgroup per 16x16 tile.  The grid is what
 // the GPU holds resident (occupancy x CUs); each wave claims 8x8-pixel tiles one at a time from a claim
 // counter (workgroup b uses counter b % 8 — the XCD the round-robin dispatch puts it on — and counter k hands
 // out tiles k, k + 8, k + 16, ... in raster order), runs the unchanged per-pixel body on the tile's 64 pixels

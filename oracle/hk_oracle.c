@@ -576,14 +576,16 @@ static Hit traverse_top(const hko_ctx* c, Counts* cnt, const Ray* ray, float max
  * DONT_EXCLUDE)`, light.wgsl:1319,1401) and the emitter BLAS walk (`traverse_bottom(..., 0.0)`,
  * light.wgsl:687).  Neither has an early exit, so the hit they return is the closest one whatever the
  * visit order, except for exact-distance ties and box tests that round across the hit distance.  The
- * HIP kernels walk the bounce ray with the G-buffer's ordered rule (closest_hit_ordered: nearer child
- * first, the farther pushed and dropped on pop once it cannot win).  hko_set_light_walk selects:
- *   HKO_WALK_REFERENCE  light.wgsl's order for both;
- *   HKO_WALK_ORDERED    the bounce walk with the ordered rule (what the HIP kernels run);
+ * HIP kernels keep light.wgsl's order for both walks; the ordered rule (closest_hit_ordered: nearer child
+ * first, the farther pushed and dropped on pop once it cannot win — the G-buffer's primary-visibility rule)
+ * is the analysed alternative for the bounce walk, bit-identical on the bench scenes and measured slower in
+ * the kernels.  hko_set_light_walk selects:
+ *   HKO_WALK_REFERENCE  light.wgsl's order for both (what the HIP kernels run);
+ *   HKO_WALK_ORDERED    the bounce walk with the ordered rule (the analysed alternative);
  *   HKO_WALK_CHECK      light.wgsl's order, and every bounce ray and emitter walk walked with the ordered rule
  *                       too; the rays whose two results differ in any bit (instance, primitive, distance, uv)
- *                       are counted (hko_light_walk_stats).  Zero bounce differences on a workload pin the
- *                       kernels' ordered bounce walk to light.wgsl's results there (tests/test_light_walks.py);
+ *                       are counted (hko_light_walk_stats).  Zero bounce differences on a workload show that
+ *                       the ordered bounce walk would return light.wgsl's results there (tests/test_light_walks.py);
  *                       the emitter count is analysis only: the kernels keep light.wgsl's order for the emitter
  *                       walk, which aims at sampled emitter points, shared triangle edges included, where the
  *                       ordered rule breaks ties differently. */

@@ -21,6 +21,8 @@ import bench  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Taa, Upscale, examples, frame_inputs  # noqa: E402
 
 CONFIGS = ["cornell-1080p-nee", "scene-1080p-full", "city-4k"]
+if len(sys.argv) > 2:
+    CONFIGS = sys.argv[2].split(",")
 
 
 def measure(config: str, wavefront: bool, warmup: int = 3, frames: int = 3) -> dict:
