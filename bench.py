@@ -39,9 +39,10 @@ import torch.distributed as dist  # noqa: E402
 
 import hikari_amd  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Taa, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import (band_gather_rows, band_of, equal_bounds, halo_rows, peer_exchange, peer_gather,  # noqa: E402
-                              reassembly_copies,  # noqa: E402
-                              rebalance, stripe_gather_rows, use_stripes)
+from hikari_amd.bands import (aligned_bounds, band_gather_rows, band_of, equal_bounds, halo_rows,  # noqa: E402
+                              peer_exchange, peer_gather, reassembly_copies, rebalance, rebalance_tiles,
+                              stripe_gather_rows, tile_gather_shape, tile_grid, tile_of, tile_reassembly_copies,
+                              use_stripes)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -296,6 +297,10 @@ def main():
     wavefront = os.environ.get("HK_BENCH_WAVEFRONT", "1" if cfg.get("wavefront") else "0") == "1"
     r.set_wavefront(wavefront)
     bounds, balance = None, []
+    # 2-D tiles (north_star: "frames tile-partition across the 8 GPUs"; bands.tile_grid: 2x2 at N = 4, 4x2 at N = 8)
+    # for the frames with neighbour reads at 4 or more ranks, HK_BENCH_DECOMP=bands keeps row bands
+    tiles = dist_on and not stripes and tile_grid(world)[1] > 1 and os.environ.get("HK_BENCH_DECOMP", "tiles") == "tiles"
+    col_bounds, my_tile, all_tiles = None, None, None
     if stripes:
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
@@ -330,6 +335,38 @@ def main():
         b = band_of(rank, world, H, bounds)
         r.resize(W, H, 1.0, b.y0, b.rows)
         band, gather_index = band_gather_rows(bounds)
+    elif tiles:
+        # cost-balanced tiles (bands.rebalance_tiles): the same calibration as the bands, each rank timing its tile
+        ny, nx = tile_grid(world)
+        bounds, col_bounds = aligned_bounds(ny, H), [aligned_bounds(nx, W)] * ny
+        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "5"))):
+            t = tile_of(rank, world, W, H, bounds, col_bounds)
+            r.resize_tile(W, H, t.x0, t.cols, t.y0, t.rows)
+            for f in range(6):
+                if f == 3:
+                    torch.cuda.synchronize()
+                    t_cal = time.perf_counter()
+                fi = frame_inputs(f, cam, lights, W, H)
+                r.render_gbuffer(fi)
+                r.render_frame(s, fi)
+                if st.denoise:
+                    r.denoise(s, fi)
+                r.tone_sum(s)
+            r.sync()
+            torch.cuda.synchronize()
+            t_cal = torch.tensor([(time.perf_counter() - t_cal) / 3.0], dtype=torch.float64,
+                                 device="cpu" if rehearsal else "cuda")
+            times = torch.zeros(world, dtype=torch.float64, device=t_cal.device)
+            dist.all_gather_into_tensor(times, t_cal)
+            times = times.cpu().numpy()
+            balance.append({"rows": list(bounds), "cols": [list(c) for c in col_bounds],
+                            "ms": [round(float(v) * 1e3, 4) for v in times]})
+            bounds, col_bounds = rebalance_tiles(bounds, col_bounds, times)
+        all_tiles = [tile_of(k, world, W, H, bounds, col_bounds) for k in range(world)]
+        my_tile = all_tiles[rank]
+        r.resize_tile(W, H, my_tile.x0, my_tile.cols, my_tile.y0, my_tile.rows)
+        tile_rows, tile_cols = tile_gather_shape(bounds, col_bounds)
+        band = tile_rows
     else:
         band = H
         r.resize(W, H, 1.0)
@@ -341,12 +378,16 @@ def main():
     # reassembly); the interleaved stripes' padded rows go into the all-gather's layout (bands.peer_gather) and are
     # put back in frame order as before.  "ring": one all-gather of the padded rows (RCCL's ring), reassembled on a
     # side stream when not already in frame order (stripes, uneven bands).
+    # Tiles: each rank's core rectangle goes into a padded (rows, cols) part of the largest tile's size, the parts are
+    # gathered per peer (bands.peer_gather, as the stripes') or by the ring all-gather, and put back in frame order by
+    # one strided copy per tile (bands.tile_reassembly_copies) on the side stream.
     gather_mode = os.environ.get("HK_BENCH_GATHER", "peer")
-    peer = dist_on and not stripes and gather_mode == "peer"
-    peer_stripes = dist_on and stripes and gather_mode == "peer"
+    peer = dist_on and not stripes and not tiles and gather_mode == "peer"
+    peer_stripes = dist_on and (stripes or tiles) and gather_mode == "peer"
     my_y0 = band_of(rank, world, H, bounds).y0 if peer else 0
-    reorder = (dist_on and not peer and not np.array_equal(gather_index, np.arange(H))
-               if (stripes or bounds is not None) else False)
+    reorder = True if tiles else ((dist_on and not peer and not np.array_equal(gather_index, np.arange(H))
+                                   if (stripes or bounds is not None) else False))
+    part_w = tile_cols if tiles else W
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
@@ -356,8 +397,8 @@ def main():
     comm = torch.cuda.Stream() if dist_on else None
     # double-buffered band / gathered frame: the all-gather of frame f runs on RCCL's stream
     # while frame f+1 renders; a buffer is reused only after its previous gather completed
-    band_t = [torch.zeros((band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] if not peer else None
-    full_t = [torch.empty((world * band, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
+    band_t = [torch.zeros((band, part_w, 4), dtype=torch.float16, device="cuda") for _ in range(2)] if not peer else None
+    full_t = [torch.empty((world * band, part_w, 4), dtype=torch.float16, device="cuda") for _ in range(2)] \
         if dist_on and not peer else None
     peer_t = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)] if peer else None
     # world size 1: the per-peer exchange sends the band to this rank itself (bands.peer_exchange self_buf), so the
@@ -371,8 +412,12 @@ def main():
 
         # one strided row copy per rank (bands.reassembly_copies); torch.index_select over the frame's row
         # indices took ~0.1 ms per 1080p frame (per-element index arithmetic), the row copies a few microseconds
-        row_copies = [reassembly_copies(frame_t[k], full_t[k], world, H, band, None if stripes else bounds)
-                      for k in range(2)] if H % 8 == 0 else None
+        if tiles:
+            row_copies = [tile_reassembly_copies(frame_t[k], full_t[k].view(world, band, part_w, 4), all_tiles)
+                          for k in range(2)]
+        else:
+            row_copies = [reassembly_copies(frame_t[k], full_t[k], world, H, band, None if stripes else bounds)
+                          for k in range(2)] if H % 8 == 0 else None
         side = torch.cuda.Stream()
         reorder_done = [None, None]
 
@@ -461,7 +506,11 @@ def main():
                 wait_all(pending[k])  # device-side: the comm stream waits for that gather
             if reorder and reorder_done[k] is not None:
                 comm.wait_event(reorder_done[k])  # full_t[k] was read by the reorder of frame f - 2
-            r.copy_output_rows(plane, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
+            if tiles:  # the core rectangle into the padded part (pitch: the part's row)
+                r.copy_output_rect(plane, core0, core_rows, my_tile.x0, my_tile.cols, band_t[k].data_ptr(),
+                                   part_w * 8, False, comm.cuda_stream)
+            else:
+                r.copy_output_rows(plane, core0, core_rows, band_t[k].data_ptr(), False, comm.cuda_stream)
             if comm_mode == "copy":
                 return
             if rehearsal:
@@ -470,7 +519,7 @@ def main():
                     wait_all(peer_gather(host, band_t[k].cpu(), rank, world))
                     full_t[k].copy_(host)
                 else:
-                    parts = [torch.empty((band, W, 4), dtype=torch.float16) for _ in range(world)]
+                    parts = [torch.empty((band, part_w, 4), dtype=torch.float16) for _ in range(world)]
                     dist.all_gather(parts, band_t[k].cpu())
                     full_t[k].copy_(torch.cat(parts))
             elif peer_stripes:
@@ -527,7 +576,11 @@ def main():
     timing = r.kernel_timing()
     # fraction of the rank's pixels with geometry (G-buffer depth > 0): background pixels take the
     # passes' early exits and move different bytes (BYTES_PER_PIXEL); read after the timed region
-    depth = r.output(11).view(np.float32).reshape(-1, 4)[:, 3]
+    depth = r.output(11).view(np.float32)
+    if tiles:  # the tile's columns + halo (the planes are full width; other columns are never computed)
+        hx = halo_rows(cfg["spatial"], cfg["denoise"])
+        depth = depth.reshape(rows, W, 4)[:, max(0, my_tile.x0 - hx): my_tile.x0 + my_tile.cols + hx]
+    depth = depth.reshape(-1, 4)[:, 3]
     coverage = float((depth >= np.finfo(np.float32).eps).mean())
     c = r.counters()
     rays = c["traverse_top"] + c["traverse_emitter"]
@@ -586,7 +639,7 @@ def main():
         source = isolated if isolated else timing
         per_frame = {k: v * launches_per_frame.get(k, 1) for k, v in source.items()}
         dom = max(per_frame, key=per_frame.get)
-        pix = W * rows
+        pix = (depth.size // rows) * rows if tiles else W * rows
         cov_px, bg_px = pix * coverage, pix * (1.0 - coverage)
         # the reference kernel's algorithmic bytes for this frame: its covered pixels' streams plus its
         # background pixels' constant stores (BYTES_PER_PIXEL (covered, background); e.g. indirect_lit_ambient
@@ -624,6 +677,7 @@ def main():
                        "rays_per_frame": int(rays // (args.steps * spp)),
                        "primary_rays_per_frame": int(primary // (args.steps * spp)),
                        "parallelism": (f"interleaved 8-row stripes x{world}" if stripes else
+                                       "cost-balanced {}x{} tiles".format(*tile_grid(world)) if tiles else
                                        f"cost-balanced row-bands x{world}") +
                                       ((" + gloo rehearsal on one GPU" if rehearsal else
                                         " + RCCL per-peer exchange" if gather_mode == "peer" else " + RCCL all-gather"))
@@ -634,6 +688,7 @@ def main():
                                         f"{gather_mode} gather)")
                                        if dist_on else "single GPU"),
                        "band_bounds": None if bounds is None else [int(v) for v in bounds],
+                       "tile_col_bounds": None if col_bounds is None else [[int(v) for v in c] for c in col_bounds],
                        "band_calibration": balance or None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -189,7 +189,11 @@ struct Frame {
     // [win_row0, win_row0 + win_rows) — a band's passes shrink their halo rows pass by pass
     // (hk_runtime.hip pass_window); 0: the whole plane
     int32_t win_row0, win_rows;
+    // column window of a 2-D tile (hk_resize_tile; win_cols > 0): the launch covers only global columns
+    // [win_col0, win_col0 + win_cols) of the full-width planes; 0: every column
+    int32_t win_col0, win_cols;
     int32_t count_y0, count_y1;    // global integrator rows whose rays are counted (the band's own rows)
+    int32_t count_x0, count_x1;    // ... and columns (a tile's own columns; the whole width otherwise)
     int32_t count_Sy0, count_Sy1;  // the same for the full-resolution G-buffer rows
     // interleaved stripes (stripe_n >= 2): the local planes hold the STRIPE_H-row stripes
     // k, k + n, k + 2n, ... of the frame (stripe_k = k) instead of one contiguous band; only for
@@ -352,6 +356,15 @@ HKD f4 load_rgba16f(const uint2* tex, int32_t idx)
 
 // Deferred-texture addressing: frame-OOB -> 0 (textureLoad robustness); in-frame rows outside
 // the band are clamped into it (those values only feed discarded halo pixels).
+// the launch's columns [win_x0, win_x1(width)) (the column window of a tile, or the whole plane width)
+HKD int32_t win_x0(const Frame& F) { return F.win_cols > 0 ? F.win_col0 : 0; }
+HKD int32_t win_x1(const Frame& F, uint32_t width) { return F.win_cols > 0 ? F.win_col0 + F.win_cols : (int32_t)width; }
+// the pixel's rays count towards this context's counters (its own rows and columns: halo pixels are another
+// context's)
+HKD bool counted(const Frame& F, int32_t x, int32_t y)
+{
+    return y >= F.count_y0 && y < F.count_y1 && x >= F.count_x0 && x < F.count_x1;
+}
 HKD bool in_frame(int32_t x, int32_t y, const uint32_t* size)
 {
     return x >= 0 && y >= 0 && (uint32_t)x < size[0] && (uint32_t)y < size[1];

@@ -91,12 +91,12 @@ HKD bool tile_pixel_at(const Frame& F, uint32_t width, int32_t row0, int32_t row
     tile_coords_at<ORDER>(bx, by, gx, gy, tx, ty);
     uint32_t t = threadIdx.x;
     uint32_t w = t >> 6, lane = t & 63u;
-    x = (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
+    x = win_x0(F) + (int32_t)(tx * 16u + (w & 1u) * 8u + (lane & 7u));
     const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0;
     const int32_t w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : rows;
     int32_t ly = w0 + (int32_t)(ty * 16u + (w >> 1) * 8u + (lane >> 3));
     y = global_row(F, ly, row0);
-    return (uint32_t)x < width && ly < w1;
+    return x < win_x1(F, width) && ly < w1;
 }
 template <int ORDER = RASTER>
 HKD bool tile_pixel(const Frame& F, uint32_t width, int32_t row0, int32_t rows, int32_t& x, int32_t& y)
@@ -110,7 +110,7 @@ HKD void tile_origin(const Frame& F, int32_t row0, int32_t& x0, int32_t& y0)
 {
     uint32_t tx, ty;
     tile_coords<ORDER>(tx, ty);
-    x0 = (int32_t)(tx * 16u);
+    x0 = win_x0(F) + (int32_t)(tx * 16u);
     y0 = row0 + (F.win_rows > 0 ? F.win_row0 : 0) + (int32_t)(ty * 16u);
 }
 constexpr int SPATIAL_ORDER = XCD_STRIPS;  // spatial reuse: neighbour reservoirs +/- 20 px in one XCD's L2
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void k_gbuffer(FrameArgs A, ViewArgs V, uint2*
             A.G.velocity_uv[idx] = make_float4(velocity.x, velocity.y, info.uv.x, info.uv.y);
         }
     }
-    if (y < A.F.count_Sy0 || y >= A.F.count_Sy1) n_primary = 0;
+    if (y < A.F.count_Sy0 || y >= A.F.count_Sy1 || x < A.F.count_x0 || x >= A.F.count_x1) n_primary = 0;
     wave_count(A.cnt.primary, n_primary);
 }
 
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_pass<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t n_top = 0, n_emitter = 0;
     if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
         direct_pass<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(256) void k_direct_fused(FrameArgs A, ChannelArgs C
             direct_body<true, false, VE, !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
         }
     }
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             direct_body<true, false, VE, !LDS>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
         }
     }
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         direct_candidate<true>(A, sc, P, D, hit, traced, n_top);
         direct_finish<true, false, false, 0>(A, sc, C1, P, D, n_top, n_emitter, nullptr, &surface);
     }
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -1374,7 +1374,7 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
         __shared__ IndStash stash;
         indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter, nullptr, nullptr, &stash);
     }
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -1395,7 +1395,8 @@ HKD void persist_tiles(const FrameArgs& A, uint32_t kind, Body body)
     const Frame& F = A.F;
     const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0;
     const int32_t w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : F.s_rows;
-    const uint32_t tiles_x = (F.s[0] + 7u) >> 3;
+    const int32_t c0 = win_x0(F), c1 = win_x1(F, F.s[0]);
+    const uint32_t tiles_x = (uint32_t)(c1 - c0 + 7) >> 3;
     const uint32_t n = tiles_x * ((uint32_t)(w1 - w0 + 7) >> 3);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t shards = gridDim.x < PERSIST_SHARDS ? gridDim.x : PERSIST_SHARDS, shard = blockIdx.x % shards;
@@ -1407,9 +1408,9 @@ HKD void persist_tiles(const FrameArgs& A, uint32_t kind, Body body)
         const uint32_t t = shard + shards * k;
         if (t >= n) break;
         const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
-        const int32_t x = (int32_t)(tx * 8u + (lane & 7u));
+        const int32_t x = c0 + (int32_t)(tx * 8u + (lane & 7u));
         const int32_t ly = w0 + (int32_t)(ty * 8u + (lane >> 3));
-        body(x, global_row(F, ly, F.s_row0), (uint32_t)x < F.s[0] && ly < w1);
+        body(x, global_row(F, ly, F.s_row0), x < c1 && ly < w1);
     }
     if (lane == 0) {
         __threadfence();
@@ -1429,7 +1430,7 @@ __global__ __launch_bounds__(256) void k_indirect_persist(FrameArgs A, ChannelAr
     persist_tiles(A, PERSIST_INDIRECT, [&](int32_t x, int32_t y, bool active) {
         uint32_t t = 0, e = 0;
         if (active) indirect_body<MULTI>(A, sc, C, x, y, t, e);
-        if (y >= A.F.count_y0 && y < A.F.count_y1) {
+        if (counted(A.F, x, y)) {
             n_top += t;
             n_emitter += e;
         }
@@ -1479,7 +1480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             direct_body<true, false, VE, 2>(A, sc, C1, P, n_top, n_emitter, nullptr, &surface);
         }
     }
-    if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+    if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
 }
@@ -1579,7 +1580,7 @@ __global__ __launch_bounds__(256) void k_wf_trace(FrameArgs A, ChannelArgs C, Wf
         int32_t x, y;
         wf_unpack(A.F, W.queue1[seg * W.seg_cap + i], x, y);
         indirect_body<false, IND_TRACE>(A, sc, C, x, y, n_top, n_emitter, &W, &key);
-        if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = 0;
+        if (!counted(A.F, x, y)) n_top = 0;
         W.keys[seg * W.seg_cap + i] = key;
     }
     (void)wf_bin_slot(W.ctl + WF_CTL_HIST + seg * W.bins, valid, key);  // the segment's histogram
@@ -1640,7 +1641,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(FrameArgs A, ChannelArgs C, Wf
         int32_t x, y;
         wf_unpack(A.F, W.queue2[i], x, y);
         indirect_body<false, IND_SHADE>(A, sc, C, x, y, n_top, n_emitter, &W);
-        if (y < A.F.count_y0 || y >= A.F.count_y1) n_top = n_emitter = 0;
+        if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     }
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -2160,7 +2161,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
     tile_coords<DENOISE_ORDER>(tx, ty);
     const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0;
     const int32_t w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : F.s_rows;
-    const int32_t x0 = (int32_t)tx * R::TW;
+    const int32_t x0 = win_x0(F) + (int32_t)tx * R::TW;
     // band row of the tile's first row: block ty / RSP, residue ty % RSP
     const int32_t ly0 = w0 + (int32_t)(ty / R::RSP) * R::TH * R::RSP + (int32_t)(ty % R::RSP);
     {
@@ -2193,7 +2194,7 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
     }
     x = x0 + tc;
     const int32_t ly = ly0 + tr * R::RSP;
-    if (x >= (int32_t)F.s[0] || ly >= w1) return;
+    if (x >= win_x1(F, F.s[0]) || ly >= w1) return;
     y = global_row(F, ly, F.s_row0);
     const int32_t idx = rb_index(F, x, y);
     const int32_t oc = (tr + rstep) * R::STRIDE + (tc + step);  // the pixel in the region
@@ -2341,7 +2342,10 @@ __global__ __launch_bounds__(256) void k_trace(Scene sc, const float* rays, cons
 // ------------------------------------------------------------------ launchers
 static dim3 tiles(uint32_t width, int32_t rows) { return dim3((width + 15u) / 16u, ((uint32_t)rows + 15u) / 16u, 1); }
 // the tile grid of a launch: its window's rows (Frame::win_rows), else the plane's
-static dim3 tiles(const Frame& F, uint32_t width, int32_t rows) { return tiles(width, F.win_rows > 0 ? F.win_rows : rows); }
+static dim3 tiles(const Frame& F, uint32_t width, int32_t rows)
+{
+    return tiles(F.win_cols > 0 ? (uint32_t)F.win_cols : width, F.win_rows > 0 ? F.win_rows : rows);
+}
 
 // LDS staging is used when the kernel's scene arrays fit LDS_SCENE_MAX and the kernel gains from
 // it.  Measured on cornell 1080p (1 x MI355X): indirect 0.370 -> 0.317 ms; direct_lit even;
@@ -2367,7 +2371,8 @@ void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32
     // A small frame (an 8- or 4-way stripe of 1080p: <= gbuffer_lds_max_px pixels, one dispatch round) is as long
     // as one wave's walk, a chain of dependent node loads: there the scene is staged in LDS with the stack after it
     // (cornell 8-way stripe ...).  A whole frame runs many rounds and stays on L2 node loads (round 1: even).
-    const bool small = (double)A.F.S[0] * (double)(A.F.win_rows > 0 ? A.F.win_rows : A.F.S_rows) <= A.opt.gbuffer_lds_max_px;
+    const bool small = (double)(A.F.win_cols > 0 ? (uint32_t)A.F.win_cols : A.F.S[0]) *
+                           (double)(A.F.win_rows > 0 ? A.F.win_rows : A.F.S_rows) <= A.opt.gbuffer_lds_max_px;
     const uint32_t scene = lds_plan_bytes(A, PLAN_GBUFFER, small);
     // (scene + stack within the LDS budget of a staged kernel)
     if (scene && shallow && scene + levels * level_bytes <= LDS_SCENE_MAX + 16384u)
@@ -2488,7 +2493,8 @@ static uint32_t persist_grid(const void* kernel, uint32_t lds, const Frame& F)
         }
     }
     const int32_t rows = F.win_rows > 0 ? F.win_rows : F.s_rows;
-    const uint32_t tiles8 = ((F.s[0] + 7u) / 8u) * (((uint32_t)rows + 7u) / 8u);
+    const uint32_t cols = F.win_cols > 0 ? (uint32_t)F.win_cols : F.s[0];
+    const uint32_t tiles8 = ((cols + 7u) / 8u) * (((uint32_t)rows + 7u) / 8u);
     const uint32_t g = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
     const uint32_t need = (tiles8 + 3u) / 4u;
     return need < g ? (need > 0u ? need : 1u) : g;
@@ -2586,7 +2592,8 @@ void launch_demod(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
 template <int C, int LEVEL>
 static void launch_level(const FrameArgs& A, const DenoiseArgs& D, hipStream_t st)
 {
-    const dim3 g = level_tiles<LEVEL>(A.F.s[0], A.F.win_rows > 0 ? A.F.win_rows : A.F.s_rows);
+    const dim3 g = level_tiles<LEVEL>(A.F.win_cols > 0 ? (uint32_t)A.F.win_cols : A.F.s[0],
+                                      A.F.win_rows > 0 ? A.F.win_rows : A.F.s_rows);
     hipLaunchKernelGGL((k_denoise3<C, LEVEL>), g, dim3(256), 0, st, A, D);
 }
 template <int C>

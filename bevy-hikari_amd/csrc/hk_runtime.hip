@@ -197,6 +197,8 @@ struct hk_ctx {
     bool bg_valid[2] = {false, false};
     // a band's per-channel row-window margins, sticky maxima since hk_resize (band_windows): -1 = none yet
     int32_t win_out = -1, win_emi = -1, win_ind = -1;
+    // a 2-D tile's own columns (hk_resize_tile): global [core_col0, core_col0 + core_cols); 0 / S.x otherwise
+    int32_t core_col0 = 0, core_cols = 0;
     int32_t bg_key[2][2] = {};
     uint8_t* gbmask = nullptr;  // the G-buffer's (ViewArgs::bg), per S pixel
     uint4* sp_view = nullptr;   // spatial view planes of the indirect channel (ChannelArgs::view), 3 x res_n
@@ -632,6 +634,11 @@ FrameArgs frame_args(hk_ctx* c, const hk_settings* st, const hk_frame_inputs* in
     F.count_Sy0 = c->S_row0 + c->core_row0;
     F.count_Sy1 = c->S_rows == (int32_t)c->S[1] && c->core_rows == (int32_t)c->s[1] ? (int32_t)c->S[1]
                                                                                       : F.count_Sy0 + c->core_rows;
+    // columns: a tile's own (ratio 1, so the same for the G-buffer), every column otherwise
+    const bool tile = c->core_cols > 0 && c->core_cols < (int32_t)c->S[0];
+    F.count_x0 = tile ? c->core_col0 : 0;
+    F.count_x1 = tile ? c->core_col0 + c->core_cols : INT32_MAX;
+    F.win_col0 = F.win_cols = 0;
     F.stripe_n = c->stripe_n;
     F.stripe_k = c->stripe_k;
     if (c->stripe_n >= 2) {  // every local row is one of this context's own rows
@@ -683,11 +690,13 @@ constexpr int32_t GBUFFER_REACH = DENOISE_OUT_REACH + SPATIAL_RANGE;
 // Only for a static frame: under camera or instance motion temporal reprojection reads the previous
 // frame's reservoirs at other rows, so every pass runs on the whole band (velocity_zero is set by
 // hk_render_gbuffer before its own window is taken, and cleared by a host G-buffer plane upload).
+bool tile_columns(const hk_ctx* c) { return c->core_cols > 0 && c->core_cols < (int32_t)c->S[0]; }
 bool band_windowed(const hk_ctx* c)
 {
-    return !(c->stripe_n >= 2 || c->core_rows >= c->s_rows || c->S_rows != c->s_rows || !c->velocity_zero ||
-             c->on(OPT_BAND_FULL_WINDOWS));
+    return !(c->stripe_n >= 2 || (c->core_rows >= c->s_rows && !tile_columns(c)) || c->S_rows != c->s_rows ||
+             !c->velocity_zero || c->on(OPT_BAND_FULL_WINDOWS));
 }
+// (a 2-D tile: the columns core +- margin as well; its planes are full width, so only the launches shrink)
 FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
 {
     if (!band_windowed(c)) return A;
@@ -695,6 +704,12 @@ FrameArgs pass_window(const hk_ctx* c, FrameArgs A, int32_t margin)
     const int32_t hi = std::min(c->s_rows, c->core_row0 + c->core_rows + margin);
     A.F.win_row0 = lo;
     A.F.win_rows = hi - lo;
+    if (tile_columns(c)) {
+        const int32_t c0 = std::max(0, c->core_col0 - margin);
+        const int32_t c1 = std::min((int32_t)c->s[0], c->core_col0 + c->core_cols + margin);
+        A.F.win_col0 = c0;
+        A.F.win_cols = c1 - c0;
+    }
     return A;
 }
 // option bg_elision = 0 switches background store elision off (the G-buffer's and the light passes'
@@ -723,6 +738,13 @@ WindowGrowth window_growth(const hk_ctx* c, const hk_settings* st)
     G.want[0] = out;
     G.want[1] = out + (st->emissive_spatial_reuse ? EMISSIVE_SPATIAL_RANGE : 0);
     G.want[2] = out + (st->indirect_spatial_reuse ? SPATIAL_RANGE : 0);
+    if (tile_columns(c)) {
+        // a 2-D tile runs every channel on its widest window from the first frame (every setting on): its window
+        // never grows, so a settings change needs no refill (the row bands' refill moves rows, not rectangles)
+        G.want[0] = DENOISE_OUT_REACH;
+        G.want[1] = DENOISE_OUT_REACH + EMISSIVE_SPATIAL_RANGE;
+        G.want[2] = DENOISE_OUT_REACH + SPATIAL_RANGE;
+    }
     const int32_t have[3] = {c->win_out, c->win_emi, c->win_ind};
     // the buffers whose records the group's window holds: spatial pairs 4/5, 8/9; direct + emissive 0-5; indirect 6-9
     static const uint32_t members[3] = {0x330u, 0x03Fu, 0x3C0u};
@@ -789,7 +811,9 @@ uint64_t gbuffer_primary_rays(const FrameArgs& A)
     const int32_t w0 = F.win_rows > 0 ? F.win_row0 : 0, w1 = F.win_rows > 0 ? F.win_row0 + F.win_rows : F.S_rows;
     if (F.stripe_n >= 2) return (uint64_t)F.S[0] * (uint64_t)(w1 - w0);
     const int32_t lo = std::max(F.S_row0 + w0, F.count_Sy0), hi = std::min(F.S_row0 + w1, F.count_Sy1);
-    return hi > lo ? (uint64_t)F.S[0] * (uint64_t)(hi - lo) : 0u;
+    const int32_t x0 = std::max(F.win_cols > 0 ? F.win_col0 : 0, F.count_x0);
+    const int32_t x1 = std::min(F.win_cols > 0 ? F.win_col0 + F.win_cols : (int32_t)F.S[0], F.count_x1);
+    return hi > lo && x1 > x0 ? (uint64_t)(x1 - x0) * (uint64_t)(hi - lo) : 0u;
 }
 
 int check_ready(hk_ctx* c, bool need_scene)
@@ -1212,11 +1236,26 @@ int hk_set_noise(hk_ctx* c, const uint8_t* rgba, uint32_t count, uint32_t size)
 }
 
 static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows,
-                       uint32_t stripe_n, uint32_t stripe_k);
+                       uint32_t stripe_n, uint32_t stripe_k, uint32_t col0 = 0u, uint32_t cols = 0u);
 
 int hk_resize(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows)
 {
     return resize_impl(c, width, height, ratio, band_y0, band_rows, 0u, 0u);
+}
+
+int hk_resize_tile(hk_ctx* c, uint32_t width, uint32_t height, uint32_t x0, uint32_t cols, uint32_t y0, uint32_t rows)
+{
+    if (!c || cols == 0 || rows == 0) return HK_ERR_INVALID;
+    if (x0 + cols > width || y0 + rows > height) return fail(c, HK_ERR_INVALID, "tile outside the frame");
+    return resize_impl(c, width, height, 1.0f, y0, rows, 0u, 0u, x0, cols);
+}
+
+int hk_tile_info(const hk_ctx* c, int32_t* col0, int32_t* cols)
+{
+    if (!c || !c->sized) return HK_ERR_STATE;
+    if (col0) *col0 = c->core_col0;
+    if (cols) *cols = c->core_cols;
+    return HK_OK;
 }
 
 int hk_resize_striped(hk_ctx* c, uint32_t width, uint32_t height, uint32_t rank, uint32_t world)
@@ -1227,9 +1266,13 @@ int hk_resize_striped(hk_ctx* c, uint32_t width, uint32_t height, uint32_t rank,
 }
 
 static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, uint32_t band_y0, uint32_t band_rows,
-                       uint32_t stripe_n, uint32_t stripe_k)
+                       uint32_t stripe_n, uint32_t stripe_k, uint32_t col0, uint32_t cols)
 {
     if (!c || width == 0 || height == 0) return HK_ERR_INVALID;
+    if (cols == 0) {
+        col0 = 0;
+        cols = width;
+    }
     (void)hipSetDevice(c->device);
     ratio = ratio < 1.0f ? 1.0f : (ratio > 2.0f ? 2.0f : ratio);  // Upscale::ratio (lib.rs:501-505)
     if (band_rows == 0) {
@@ -1239,6 +1282,8 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     if (band_y0 + band_rows > height) return fail(c, HK_ERR_INVALID, "band outside the frame");
     bool whole = band_y0 == 0 && band_rows == height;
     if (!whole && ratio != 1.0f) return fail(c, HK_ERR_INVALID, "row bands require upscale ratio 1.0");
+    const bool tile_cols = cols < width;
+    if (tile_cols && (ratio != 1.0f || stripe_n >= 2)) return fail(c, HK_ERR_INVALID, "tiles require upscale ratio 1.0");
     uint32_t stripe_rows = 0;  // rows of stripes k, k + n, ... (STRIPE_H rows each, the last one may be short)
     if (stripe_n >= 2) {
         if (stripe_n > (height + STRIPE_H - 1) / STRIPE_H)
@@ -1261,6 +1306,8 @@ static int resize_impl(hk_ctx* c, uint32_t width, uint32_t height, float ratio, 
     c->s[1] = (uint32_t)std::ceil(scale * (float)height);
     c->stripe_n = (int32_t)stripe_n;
     c->stripe_k = (int32_t)stripe_k;
+    c->core_col0 = (int32_t)col0;
+    c->core_cols = (int32_t)cols;
     if (stripe_n >= 2) {
         c->S_row0 = c->s_row0 = 0;
         c->S_rows = c->s_rows = (int32_t)stripe_rows;
@@ -2121,7 +2168,24 @@ int hk_get_output(hk_ctx* c, int id, void* dst, size_t bytes, int to_host, void*
     return HK_OK;
 }
 
+static int copy_output_rect(hk_ctx* c, int id, uint32_t row0, uint32_t rows, uint32_t col0, uint32_t cols, void* dst,
+                            size_t dst_pitch, int to_host, void* stream);
+
 int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* dst, int to_host, void* stream)
+{
+    return copy_output_rect(c, id, row0, rows, 0u, 0u, dst, 0u, to_host, stream);
+}
+
+int hk_copy_output_rect(hk_ctx* c, int id, uint32_t row0, uint32_t rows, uint32_t col0, uint32_t cols, void* dst,
+                        size_t dst_pitch, int to_host, void* stream)
+{
+    if (cols == 0) return HK_ERR_INVALID;
+    return copy_output_rect(c, id, row0, rows, col0, cols, dst, dst_pitch, to_host, stream);
+}
+
+// cols 0: whole rows (hk_copy_output_rows); dst_pitch 0: the rectangle's own row bytes
+static int copy_output_rect(hk_ctx* c, int id, uint32_t row0, uint32_t rows, uint32_t col0, uint32_t cols, void* dst,
+                            size_t dst_pitch, int to_host, void* stream)
 {
     if (!c || !dst) return HK_ERR_INVALID;
     if (!c->sized) return fail(c, HK_ERR_STATE, "hk_resize has not been called");
@@ -2129,6 +2193,13 @@ int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* d
     void* p = output_ptr(c, id, &w, &h, &b);
     if (!p) return fail(c, HK_ERR_INVALID, "unknown output id");
     if (row0 + rows > h) return fail(c, HK_ERR_INVALID, "row range outside the plane");
+    if (cols == 0) {
+        col0 = 0;
+        cols = w;
+    }
+    if (col0 + cols > w) return fail(c, HK_ERR_INVALID, "column range outside the plane");
+    if (dst_pitch == 0) dst_pitch = (size_t)cols * b;
+    if (dst_pitch < (size_t)cols * b) return fail(c, HK_ERR_INVALID, "destination pitch below the rectangle's row bytes");
     (void)hipSetDevice(c->device);
     // A copy on a stream other than the frame sequence's (a communication stream) enqueues nothing on the
     // frame stream but, when the plane's producer may have run there, an event marker: the frame stream
@@ -2148,8 +2219,12 @@ int hk_copy_output_rows(hk_ctx* c, int id, uint32_t row0, uint32_t rows, void* d
         }
     }
     size_t pitch = (size_t)w * b;
-    HK_HIP(c, hipMemcpyAsync(dst, (const char*)p + (size_t)row0 * pitch, (size_t)rows * pitch,
-                             to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, st));
+    const hipMemcpyKind kind = to_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    const char* src = (const char*)p + (size_t)row0 * pitch + (size_t)col0 * b;
+    if (cols == w && dst_pitch == pitch)
+        HK_HIP(c, hipMemcpyAsync(dst, src, (size_t)rows * pitch, kind, st));
+    else
+        HK_HIP(c, hipMemcpy2DAsync(dst, dst_pitch, src, pitch, (size_t)cols * b, rows, kind, st));
     if (to_host) HK_HIP(c, hipStreamSynchronize(st));
     if (foreign) {
         // entries whose copies have completed go back to the pool (a plane nobody rewrites would otherwise keep its

@@ -152,6 +152,9 @@ def lib() -> C.CDLL:
         "hk_resize_striped": (i32, [vp, u32, u32, u32, u32]),
         "hk_band_info": (i32, [vp] + [C.POINTER(C.c_int32)] * 4),
         "hk_band_window_grow": (i32, [vp, C.POINTER(hk_settings), vp, i32]),
+        "hk_resize_tile": (i32, [vp, u32, u32, u32, u32, u32, u32]),
+        "hk_tile_info": (i32, [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+        "hk_copy_output_rect": (i32, [vp, i32, u32, u32, u32, u32, vp, C.c_size_t, i32, vp]),
         "hk_reservoir_rows": (i32, [vp, i32, C.c_int32, C.c_int32, vp, i32, vp]),
         "hk_copy_output_rows": (i32, [vp, i32, u32, u32, vp, i32, vp]),
         "hk_render_gbuffer": (i32, [vp, C.POINTER(hk_frame_inputs), vp]),
@@ -202,7 +205,7 @@ def lib() -> C.CDLL:
 EXPORTED_SYMBOLS = [
     "hk_abi_version", "hk_create", "hk_destroy", "hk_last_error", "hk_settings_default", "hk_set_option",
     "hk_get_option", "hk_option_name", "hk_scene_upload",
-    "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_band_window_grow", "hk_reservoir_rows", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
+    "hk_set_noise", "hk_texture_upload", "hk_resize", "hk_resize_striped", "hk_set_band_halo", "hk_band_info", "hk_band_window_grow", "hk_reservoir_rows", "hk_resize_tile", "hk_tile_info", "hk_copy_output_rect", "hk_copy_output_rows", "hk_render_gbuffer", "hk_set_gbuffer_plane", "hk_render_frame",
     "hk_denoise", "hk_tone_sum", "hk_update_instances", "hk_read_scene_array", "hk_post_process", "hk_accumulate", "hk_resolve_accumulation", "hk_output_info", "hk_get_output", "hk_output_device_ptr", "hk_sync", "hk_set_wavefront", "hk_lane_stats", "hk_dump_reservoirs",
     "hk_load_reservoirs", "hk_reset_counters", "hk_read_counters", "hk_enable_kernel_timing", "hk_kernel_timing", "hk_set_kernel_timing_interval",
     "hk_trace", "hk_selftest_f16", "hk_selftest_div", "hk_selftest_rcp", "hks_create", "hks_destroy", "hks_last_error", "hks_add_mesh", "hks_add_material",

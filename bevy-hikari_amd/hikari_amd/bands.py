@@ -93,6 +93,70 @@ def band_gather_rows(bounds) -> tuple:
     return pad, index
 
 
+# ---------------------------------------------------------------- 2-D tiles
+# north_star: "frames tile-partition across the 8 GPUs".  A rank renders a tile — columns [x0, x0 + cols) of rows
+# [y0, y0 + rows) — plus a halo on every side (hk_resize_tile): its planes hold the band's rows at full width and every
+# pass runs only on the rows and columns later passes read, so the tile's own pixels equal a whole-frame render.  At
+# N = 8 the frame is 4 row bands x 2 column bands: a 4K tile of 1920 x 540 recomputes (540 + 2 x 36) rows x (1920 + 36)
+# columns for its G-buffer and indirect temporal pass (1.15x) where a 270-row band recomputes 342 x 3840 (1.27x); for
+# scene 1080p's narrow balanced bands the saving is larger.
+@dataclass(frozen=True)
+class Tile:
+    rank: int
+    world: int
+    x0: int    # first global column of the tile
+    cols: int
+    y0: int    # first global row
+    rows: int
+
+
+def tile_grid(world: int) -> tuple:
+    """(row bands, column bands) of a world-rank tiling: two columns once there are 4 or more (even) ranks."""
+    nx = 2 if world >= 4 and world % 2 == 0 else 1
+    return world // nx, nx
+
+
+def tile_of(rank: int, world: int, width: int, height: int, row_bounds=None, col_bounds=None) -> Tile:
+    """Rank's tile: row band rank // nx of `row_bounds` (equal 8-aligned bands by default), column band rank % nx of
+    col_bounds[row band] (equal halves by default; cost-balanced per row band by rebalance_tiles)."""
+    ny, nx = tile_grid(world)
+    ty, tx = divmod(rank, nx)
+    rb = list(row_bounds) if row_bounds is not None else aligned_bounds(ny, height)
+    cb = list(col_bounds[ty]) if col_bounds is not None else aligned_bounds(nx, width)
+    if len(rb) != ny + 1 or len(cb) != nx + 1:
+        raise ValueError("bounds do not match the tile grid")
+    return Tile(rank, world, int(cb[tx]), int(cb[tx + 1] - cb[tx]), int(rb[ty]), int(rb[ty + 1] - rb[ty]))
+
+
+def aligned_bounds(n: int, size: int, align: int = BAND_ALIGN) -> list:
+    """n near-equal parts of `size` with inner boundaries on multiples of `align`."""
+    return [0] + [int(round(k * size / n / align)) * align for k in range(1, n)] + [size]
+
+
+def rebalance_tiles(row_bounds, col_bounds, times, align: int = BAND_ALIGN):
+    """New (row_bounds, col_bounds) from per-tile times (rank order): the row bands get equal shares of their
+    slowest tile's time x tiles (rebalance over rows), and inside every row band the column boundary moves to equal
+    tile times (rebalance over that band's columns)."""
+    ny, nx = len(row_bounds) - 1, len(col_bounds[0]) - 1
+    t = np.asarray(times, np.float64).reshape(ny, nx)
+    new_rows = rebalance(row_bounds, t.max(axis=1) * nx, align)
+    new_cols = [rebalance(col_bounds[j], t[j], align) if nx > 1 else list(col_bounds[j]) for j in range(ny)]
+    return new_rows, new_cols
+
+
+def tile_gather_shape(row_bounds, col_bounds) -> tuple:
+    """(rows, cols) every rank contributes to the gather of tiles: the largest tile (smaller ones zero-padded)."""
+    rows = int(np.diff(np.asarray(row_bounds)).max())
+    cols = int(max(np.diff(np.asarray(c)).max() for c in col_bounds))
+    return rows, cols
+
+
+def tile_reassembly_copies(frame, gathered, tiles) -> list:
+    """(destination, source) views putting a gather of padded tiles back in frame order: frame (H, W, C), gathered
+    (world, rows_max, cols_max, C); tiles: the Tile of every rank."""
+    return [(frame[t.y0: t.y0 + t.rows, t.x0: t.x0 + t.cols], gathered[t.rank, : t.rows, : t.cols]) for t in tiles]
+
+
 # ---------------------------------------------------------------- interleaved stripes
 # Frames without neighbour reads (spatial reuse and denoise off, halo 0) are split into 8-row
 # stripes dealt round-robin to the ranks (hk_resize_striped): every rank gets an equal share of

@@ -112,6 +112,21 @@ class HikariRenderer:
         _check(self.ctx, self._L.hk_resize_striped(self.ctx, width, height, rank, world), "hk_resize_striped")
         self.width, self.height = width, height
 
+    def resize_tile(self, width: int, height: int, x0: int, cols: int, y0: int, rows: int) -> None:
+        """A 2-D tile of the frame: columns [x0, x0 + cols) of rows [y0, y0 + rows) plus halo (hk_resize_tile)."""
+        _check(self.ctx, self._L.hk_resize_tile(self.ctx, width, height, x0, cols, y0, rows), "hk_resize_tile")
+        self.width, self.height = width, height
+
+    def tile_info(self):
+        v = [C.c_int32(), C.c_int32()]
+        _check(self.ctx, self._L.hk_tile_info(self.ctx, C.byref(v[0]), C.byref(v[1])), "hk_tile_info")
+        return v[0].value, v[1].value
+
+    def copy_output_rect(self, output_id: int, row0: int, rows: int, col0: int, cols: int, dst_ptr: int,
+                         dst_pitch: int = 0, to_host: bool = False, stream=None) -> None:
+        _check(self.ctx, self._L.hk_copy_output_rect(self.ctx, output_id, row0, rows, col0, cols, dst_ptr, dst_pitch,
+                                                     int(to_host), _stream(stream)), "hk_copy_output_rect")
+
     def set_band_halo(self, rows: int) -> None:
         _check(self.ctx, self._L.hk_set_band_halo(self.ctx, rows), "hk_set_band_halo")
 

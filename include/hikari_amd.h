@@ -291,6 +291,17 @@ int hk_resize_striped(hk_ctx* ctx, uint32_t width, uint32_t height, uint32_t ran
  * reuse + 4 a-trous levels + the variance blur: 20 + 15 + 1); 0 is exact when spatial reuse and
  * denoise are both off.  Call before hk_resize. */
 int hk_set_band_halo(hk_ctx* ctx, uint32_t rows);
+/* 2-D tile decomposition for N GPUs (no reference counterpart; north_star: "frames tile-partition across the 8
+ * GPUs"): the context renders the frame's columns [x0, x0 + cols) of rows [y0, y0 + rows) plus a halo of
+ * hk_set_band_halo pixels on every side (upscale ratio 1.0).  The planes hold the band's rows (rows + halo) at full
+ * width; every pass runs only on the columns and rows the later passes read (core +- its reach), so the core
+ * rectangle is bit-identical to a whole-frame render for a static camera.  Each channel runs on its widest window
+ * from the first frame, so settings changes need no refill (hk_band_window_grow lists nothing).  Ray counters count
+ * the core rectangle only. */
+int hk_resize_tile(hk_ctx* ctx, uint32_t width, uint32_t height, uint32_t x0, uint32_t cols, uint32_t y0,
+                   uint32_t rows);
+/* a tile's own columns (global); 0 and the frame width for row bands and whole frames */
+int hk_tile_info(const hk_ctx* ctx, int32_t* col0, int32_t* cols);
 /* band geometry after hk_resize: local rows [0, rows) hold global rows [row0, row0+rows);
  * the band's own (non-halo) rows are local [core_row0, core_row0+core_rows) */
 int hk_band_info(const hk_ctx* ctx, int32_t* row0, int32_t* rows, int32_t* core_row0, int32_t* core_rows);
@@ -358,6 +369,10 @@ int hk_set_wavefront(hk_ctx* ctx, int enable);
  * frame stream itself never waits for the copy or for what follows it on `stream`. */
 int hk_copy_output_rows(hk_ctx* ctx, int output_id, uint32_t row0, uint32_t rows, void* dst, int to_host,
                         void* stream);
+/* the same for the rectangle of band-local rows [row0, row0+rows) x columns [col0, col0+cols) (a tile's core rows and
+ * columns), written with row pitch dst_pitch bytes (0: cols x bytes per pixel, packed) */
+int hk_copy_output_rect(hk_ctx* ctx, int output_id, uint32_t row0, uint32_t rows, uint32_t col0, uint32_t cols,
+                        void* dst, size_t dst_pitch, int to_host, void* stream);
 /* copy reservoir buffer `id` (0..9) in the reference's AoS PackedReservoir layout */
 int hk_dump_reservoirs(hk_ctx* ctx, int id, hk_packed_reservoir* dst, size_t count, void* stream);
 int hk_load_reservoirs(hk_ctx* ctx, int id, const hk_packed_reservoir* src, size_t count, void* stream);

@@ -161,6 +161,7 @@ struct hko_ctx {
     uint16_t* taa_buf[2]; uint32_t taa_wh[2];
     hk_counters counters;
     int32_t band_y0, band_y1; /* rows computed by every pass (whole frame by default) */
+    int32_t band_x0, band_x1; /* ... and columns (hko_set_tile; the whole width by default) */
     int32_t stripe_n, stripe_k; /* hko_set_stripes: only rows of 8-row stripes k, k + n, ... (n >= 2) */
     /* the closest-hit light walks (the indirect bounce, light.wgsl:1319,1401; the emitter BLAS walk of
      * select_light_candidate, light.wgsl:687): hko_set_light_walk */
@@ -1991,6 +1992,8 @@ hko_ctx* hko_create(const hk_scene_desc* sc, const uint8_t* noise, uint32_t widt
     c->threads = threads;
     c->band_y0 = 0;
     c->band_y1 = (int32_t)height;
+    c->band_x0 = 0;
+    c->band_x1 = (int32_t)width;
     size_t S = (size_t)width * height, s = (size_t)c->s[0] * c->s[1];
     c->g_position = (float*)calloc(S * 4, sizeof(float));
     c->g_normal = (uint32_t*)calloc(S, sizeof(uint32_t));
@@ -2108,7 +2111,7 @@ void hko_render_gbuffer(hko_ctx* c, const hk_frame_inputs* in)
         for (int32_t y = c->band_y0; y < c->band_y1; ++y)
             {
                 if (!row_on(c, y)) continue;
-                for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) gbuffer_pixel(c, &k, in, &G, x, y);
+                for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->S[0] ? c->band_x1 : (int32_t)c->S[0]); ++x) gbuffer_pixel(c, &k, in, &G, x, y);
             }
         add_counts(c, &k);
     }
@@ -2149,7 +2152,7 @@ static void run_pass(hko_ctx* c, const Pass* P, Kind kind)
         for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
         {
             if (!row_on(c, y)) continue;
-            for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) {
+            for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->s[0] ? c->band_x1 : (int32_t)c->s[0]); ++x) {
 #ifdef HKO_STATS
                 hko_npix = c->s[0] * c->s[1];
                 hko_pixel = (int32_t)(x + (int32_t)c->s[0] * y);
@@ -2183,7 +2186,7 @@ void hko_render_frame(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* 
     for (int32_t y = c->band_y0; y < c->band_y1; ++y)
         {
             if (!row_on(c, y)) continue;
-            for (int32_t x = 0; x < (int32_t)c->S[0]; ++x) full_screen_albedo(&P, x, y);
+            for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->S[0] ? c->band_x1 : (int32_t)c->S[0]); ++x) full_screen_albedo(&P, x, y);
         }
 
     uint32_t current = P.number % 2u, previous = 1u - current;
@@ -2233,7 +2236,7 @@ void hko_denoise(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
         for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
             {
                 if (!row_on(c, y)) continue;
-                for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) demodulation(&D, x, y);
+                for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->s[0] ? c->band_x1 : (int32_t)c->s[0]); ++x) demodulation(&D, x, y);
             }
         for (int level = 0; level < 4; ++level) {
             D.level = level;
@@ -2241,7 +2244,7 @@ void hko_denoise(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* in)
             for (int32_t y = c->band_y0; y < (c->band_y1 < (int32_t)c->s[1] ? c->band_y1 : (int32_t)c->s[1]); ++y)
                 {
                     if (!row_on(c, y)) continue;
-                    for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) denoise_pixel(&D, x, y);
+                    for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->s[0] ? c->band_x1 : (int32_t)c->s[0]); ++x) denoise_pixel(&D, x, y);
                 }
         }
     }
@@ -2311,10 +2314,10 @@ void hko_post_process(hko_ctx* c, const hk_settings* st, const hk_frame_inputs* 
         I.output.data = c->upscale, I.output.w = U0, I.output.h = U1;
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
         for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
-            for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) hk_pp_smaa_tu4x(&F, &I, x, y);
+            for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->s[0] ? c->band_x1 : (int32_t)c->s[0]); ++x) hk_pp_smaa_tu4x(&F, &I, x, y);
 #pragma omp parallel for schedule(static) HKO_THREADS(c)
         for (int32_t y = 0; y < (int32_t)c->s[1]; ++y)
-            for (int32_t x = 0; x < (int32_t)c->s[0]; ++x) hk_pp_smaa_extrapolate(&I.output, x, y);
+            for (int32_t x = c->band_x0; x < (c->band_x1 < (int32_t)c->s[0] ? c->band_x1 : (int32_t)c->s[0]); ++x) hk_pp_smaa_extrapolate(&I.output, x, y);
         taa_input = pp_tex(c->upscale, U0, U1, 1, 4);
     }
     if (st->taa == 0u) {
@@ -2376,6 +2379,15 @@ void hko_set_band(hko_ctx* c, int32_t y0, int32_t rows, int32_t halo)
     int32_t a = y0 - halo, b = y0 + rows + halo;
     c->band_y0 = a < 0 ? 0 : a;
     c->band_y1 = b > (int32_t)c->S[1] ? (int32_t)c->S[1] : b;
+}
+
+/* a 2-D tile (hk_resize_tile): columns [x0, x0 + cols) of rows [y0, y0 + rows), plus halo on every side */
+void hko_set_tile(hko_ctx* c, int32_t x0, int32_t cols, int32_t y0, int32_t rows, int32_t halo)
+{
+    hko_set_band(c, y0, rows, halo);
+    int32_t a = x0 - halo, b = x0 + cols + halo;
+    c->band_x0 = a < 0 ? 0 : a;
+    c->band_x1 = b > (int32_t)c->S[0] ? (int32_t)c->S[0] : b;
 }
 
 void hko_set_stripes(hko_ctx* c, int32_t rank, int32_t world)

@@ -39,6 +39,7 @@ int hko_set_textures(hko_ctx* ctx, const hk_texture* textures, uint32_t count);
 void hko_sample_texture(const hko_ctx* ctx, uint32_t id, const float* uv, uint32_t n, float* out);
 /* restrict every pass to rows [y0 - halo, y0 + rows + halo) (multi-rank band tests; ratio 1) */
 void hko_set_band(hko_ctx* ctx, int32_t y0, int32_t rows, int32_t halo);
+void hko_set_tile(hko_ctx* ctx, int32_t x0, int32_t cols, int32_t y0, int32_t rows, int32_t halo);
 /* compute only the rows of the 8-row stripes rank, rank + world, ... (hk_resize_striped; passes
  * without neighbour reads only) */
 void hko_set_stripes(hko_ctx* ctx, int32_t rank, int32_t world);

@@ -34,6 +34,7 @@ def lib() -> C.CDLL:
         "hko_create": (vp, [vp, vp, u32, u32, f, C.c_int]),
         "hko_destroy": (None, [vp]),
         "hko_set_band": (None, [vp, C.c_int32, C.c_int32, C.c_int32]),
+        "hko_set_tile": (None, [vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
         "hko_set_stripes": (None, [vp, C.c_int32, C.c_int32]),
         "hko_render_gbuffer": (None, [vp, vp]),
         "hko_set_scene": (None, [vp, vp]),
@@ -132,6 +133,10 @@ class Oracle:
 
     def set_band(self, y0: int, rows: int, halo: int = 40):
         self._L.hko_set_band(self.ctx, y0, rows, halo)
+
+    def set_tile(self, x0: int, cols: int, y0: int, rows: int, halo: int = 40):
+        """Compute only a 2-D tile plus its halo on every side (hk_resize_tile's pixels)."""
+        self._L.hko_set_tile(self.ctx, x0, cols, y0, rows, halo)
 
     def set_stripes(self, rank: int, world: int):
         """Compute only this rank's 8-row stripes (hk_resize_striped's rows)."""

@@ -84,16 +84,18 @@ CITY_UNEVEN = [0, 464, 848, 1104, 1296, 1488, 1688, 1904, 2160]
 
 
 @pytest.mark.parametrize("config,frames,uneven", [("cornell-1080p-nee", 4, False), ("scene-1080p-full", 2, False),
-                                                  ("city-4k", 2, False), ("city-4k", 2, True)],
-                         ids=["cornell-1080p-nee-4", "scene-1080p-full-2", "city-4k-2", "city-4k-uneven-2"])
+                                                  ("city-4k", 2, False), ("city-4k", 2, True), ("city-4k", 2, "tiles")],
+                         ids=["cornell-1080p-nee-4", "scene-1080p-full-2", "city-4k-2", "city-4k-uneven-2",
+                              "city-4k-tiles-2"])
 def test_full_size_bench_workloads_bit_exact(config, frames, uneven):
     """The bench workloads themselves (BASELINE configs 2-4 at 1920x1080 and 3840x2160): every output plane
     of every frame, all reservoir buffers of the last frame and the ray counters bit-exact; for city 4K
     the 8-band decomposition of configs[3] too (each band's core rows of the tone-mapped frame), with
-    equal bands and with uneven (cost-balanced) ones."""
+    equal bands and with uneven (cost-balanced) ones, and the 8-tile one (4 row bands x 2 column bands of
+    1920 x 540, hk_resize_tile: each tile's core rectangle, and the tiles' ray counts summing to the frame's)."""
     import bench
     from hikari_amd import HikariRenderer, HikariSettings, Upscale, frame_inputs
-    from hikari_amd.bands import band_of, halo_rows
+    from hikari_amd.bands import band_of, halo_rows, tile_of
     cfg = bench.CONFIGS[config]
     w, h = cfg["width"], cfg["height"]
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=cfg["spatial"], denoise=cfg["denoise"])
@@ -104,12 +106,15 @@ def test_full_size_bench_workloads_bit_exact(config, frames, uneven):
     bands = []
     if config == "city-4k":
         for k in range(8):
-            b = band_of(k, 8, h, CITY_UNEVEN if uneven else None)
+            b = tile_of(k, 8, w, h) if uneven == "tiles" else band_of(k, 8, h, CITY_UNEVEN if uneven else None)
             rb = HikariRenderer(0)
             rb.set_noise()
             rb.upload_scene(scene)
             rb.set_band_halo(halo_rows(cfg["spatial"], cfg["denoise"]))
-            rb.resize(w, h, 1.0, b.y0, b.rows)
+            if uneven == "tiles":
+                rb.resize_tile(w, h, b.x0, b.cols, b.y0, b.rows)
+            else:
+                rb.resize(w, h, 1.0, b.y0, b.rows)
             bands.append((b, rb))
     errors = []
     for f in range(frames):
@@ -123,8 +128,15 @@ def test_full_size_bench_workloads_bit_exact(config, frames, uneven):
         for b, rb in bands:
             row0, rows, core0, core_rows = rb.band_info()
             assert row0 + core0 == b.y0 and core_rows == b.rows == (b.rows if uneven else h // 8)
-            m = mismatch_report(canon_plane(10, rb.output(10)[core0: core0 + core_rows]), whole[b.y0: b.y0 + b.rows],
-                                f"frame {f} band {b.y0}+{b.rows} output 10")
+            if uneven == "tiles":
+                assert rb.tile_info() == (b.x0, b.cols)
+                x0, x1 = b.x0, b.x0 + b.cols
+                mine = canon_plane(10, np.ascontiguousarray(rb.output(10)[core0: core0 + core_rows, x0:x1]))
+                ref = canon_plane(10, np.ascontiguousarray(o.output(10)[b.y0: b.y0 + b.rows, x0:x1]))
+            else:
+                mine = canon_plane(10, rb.output(10)[core0: core0 + core_rows])
+                ref = whole[b.y0: b.y0 + b.rows]
+            m = mismatch_report(mine, ref, f"frame {f} band {b.y0}+{b.rows} output 10")
             if m:
                 errors.append(m)
         for oid in OUTPUTS:
@@ -140,6 +152,9 @@ def test_full_size_bench_workloads_bit_exact(config, frames, uneven):
             errors.append(m)
     assert not errors, "\n".join(errors[:20])
     assert r.counters() == o.counters()
+    if uneven == "tiles":  # the tiles count their own pixels' rays: together the frames' rays, once each
+        total = {k: sum(rb.counters()[k] for _, rb in bands) for k in ("traverse_top", "traverse_emitter", "primary")}
+        assert total == o.counters(), (total, o.counters())
 
 
 @pytest.mark.parametrize("denoise,mode", [(True, "forced"), (False, "forced"), (True, "serial")],
@@ -411,6 +426,87 @@ def test_gpu_row_bands_settings_toggle(refill):
         # the widening frames moved rows (both inner bands on both sides, the outer bands on one side)
         grown = dict(moved)
         assert grown[0] == 0 and grown[4] > 0 and grown[6] > 0 and grown[8] == 0 and grown[9] == 0, moved
+
+
+@pytest.mark.parametrize("world,spatial,denoise", [(4, True, True), (8, True, True), (4, "indirect", True),
+                                                   (8, False, False)])
+def test_gpu_tiles_match_whole_frame(world, spatial, denoise):
+    """2-D tile contexts (hk_resize_tile: 2x2 at world 4, 4x2 at world 8 on a 128 x 192 frame, halo 40) reproduce the
+    whole-frame oracle render bit-exactly on their own rectangles over 5 frames, and their ray counters add up to the
+    whole frame's (each pixel counted by the tile that owns it).  The tiles' rows + halo and columns + halo are strict
+    parts of the frame, so every pass runs on a proper row and column window (pass_window)."""
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs, load_noise
+    from hikari_amd.bands import halo_rows, tile_of
+    from oracle import Oracle
+    W, H = 128, 192
+    scene, cam, lights = examples.cornell()
+    desc = scene.build()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=bool(spatial),
+                        emissive_spatial_reuse=spatial is True, denoise=denoise)
+    s = st.to_c()
+    o = Oracle(desc, load_noise(), W, H, 1.0)
+    ranks = []
+    for k in range(world):
+        t = tile_of(k, world, W, H)
+        r = HikariRenderer(0)
+        r.set_noise()
+        r.upload_scene(scene)
+        r.set_band_halo(halo_rows(True, True))
+        r.resize_tile(W, H, t.x0, t.cols, t.y0, t.rows)
+        ranks.append((t, r))
+    errors = []
+    for f in range(5):
+        fi = frame_inputs(f, cam, lights, W, H)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.denoise(s, fi)
+        o.tone_sum(s)
+        whole = o.output(10)
+        for t, r in ranks:
+            r.render_gbuffer(fi)
+            r.render_frame(s, fi)
+            r.denoise(s, fi)
+            r.tone_sum(s)
+            row0, rows, core0, core_rows = r.band_info()
+            assert row0 + core0 == t.y0 and core_rows == t.rows
+            mine = np.ascontiguousarray(r.output(10)[core0: core0 + core_rows, t.x0: t.x0 + t.cols])
+            ref = np.ascontiguousarray(whole[t.y0: t.y0 + t.rows, t.x0: t.x0 + t.cols])
+            if not np.array_equal(canon_plane(10, mine), canon_plane(10, ref)):
+                errors.append(f"frame {f} tile {t}")
+    assert not errors, "\n".join(errors)
+    total = {"traverse_top": 0, "traverse_emitter": 0, "primary": 0}
+    for _, r in ranks:
+        for k, v in r.counters().items():
+            total[k] += v
+    assert total == o.counters()
+
+
+def test_gpu_tile_rect_copy():
+    """hk_copy_output_rect: a tile's core rectangle of the tone-mapped plane copied packed and into a pitched
+    whole-frame buffer equals those pixels of hk_get_output."""
+    from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs
+    W, H = 128, 96
+    scene, cam, lights = examples.cornell()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0).to_c()
+    r = HikariRenderer(0)
+    r.set_noise()
+    r.upload_scene(scene)
+    r.set_band_halo(16)
+    r.resize_tile(W, H, 64, 64, 48, 48)
+    fi = frame_inputs(0, cam, lights, W, H)
+    r.render_gbuffer(fi)
+    r.render_frame(st, fi)
+    r.tone_sum(st)
+    full = r.output(10)
+    row0, rows, core0, core_rows = r.band_info()
+    packed = np.zeros((core_rows, 64, 8), np.uint8)
+    r.copy_output_rect(10, core0, core_rows, 64, 64, packed.ctypes.data, 0, True)
+    assert np.array_equal(packed, full[core0: core0 + core_rows, 64:128])
+    frame = np.zeros((H, W, 8), np.uint8)
+    dst = frame[48:96, 64:128]
+    r.copy_output_rect(10, core0, core_rows, 64, 64, dst.ctypes.data, W * 8, True)
+    assert np.array_equal(frame[48:96, 64:128], full[core0: core0 + core_rows, 64:128])
+    assert not frame[:48].any() and not frame[:, :64].any()
 
 
 def test_gpu_row_bands_moving_camera_within_tolerance():

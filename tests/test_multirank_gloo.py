@@ -487,3 +487,114 @@ def test_band_window_refill_exchange(bounds):
         fake.check()
     assert moved == sum(got for _, got, _ in res) > 0
 
+
+
+TW, TH = 128, 128
+
+
+def _tile_render(tile=None, counters=False):
+    from oracle import Oracle
+
+    from hikari_amd import HikariSettings, Upscale, examples, frame_inputs, load_noise
+    scene, cam, lights = examples.cornell()
+    desc = scene.build()
+    st = HikariSettings(upscale=Upscale.SMAA_TU_1_0, indirect_spatial_reuse=True, denoise=True)
+    s = st.to_c()
+    o = Oracle(desc, load_noise(), TW, TH, 1.0, threads=2)
+    if tile is not None:
+        o.set_tile(tile.x0, tile.cols, tile.y0, tile.rows, 40)
+    for f in range(3):
+        fi = frame_inputs(f, cam, lights, TW, TH)
+        o.render_gbuffer(fi)
+        o.render_frame(s, fi)
+        o.denoise(s, fi)
+        o.tone_sum(s)
+    img = o.output(10)
+    c = o.counters()
+    o.close()
+    return (img, c) if counters else img
+
+
+def _tile_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    for p in (root / "bevy-hikari_amd", root / "oracle", root / "tests"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    from hikari_amd.bands import aligned_bounds, tile_gather_shape, tile_grid, tile_of
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ny, nx = tile_grid(world)
+        rb, cb = aligned_bounds(ny, TH), [aligned_bounds(nx, TW)] * ny
+        t = tile_of(rank, world, TW, TH, rb, cb)
+        img, cnt = _tile_render(t, counters=True)
+        rows, cols = tile_gather_shape(rb, cb)
+        mine = np.zeros((rows, cols, 8), np.uint8)
+        mine[: t.rows, : t.cols] = img[t.y0: t.y0 + t.rows, t.x0: t.x0 + t.cols]
+        full = torch.empty((world * rows, cols, 8), dtype=torch.uint8)
+        dist.all_gather_into_tensor(full, torch.from_numpy(mine))
+        n = torch.tensor([cnt["traverse_top"], cnt["traverse_emitter"], cnt["primary"]], dtype=torch.int64)
+        dist.all_reduce(n)
+        if rank == 0:
+            q.put((full.numpy().reshape(world, rows, cols, 8).copy(), n.tolist(), None))
+    except Exception as e:  # reported through the queue
+        q.put((None, None, repr(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_tiles_reassemble_whole_frame():
+    """2-D tiles (hk_resize_tile's decomposition, north_star "frames tile-partition across the GPUs"): 4 gloo ranks
+    each render a 64x64 tile of a 128x128 frame plus a 40-pixel halo on every side with their own oracle context
+    (hko_set_tile: only those rows and columns computed), all-gather the padded tiles and reassemble them
+    (bands.tile_reassembly_copies): the frame equals the whole-frame render (spatial reuse and the denoiser on).  (The
+    oracle counts the halo's rays too; the GPU tile test checks that the contexts count only their own pixels.)"""
+    import torch
+    import torch.multiprocessing as mp
+
+    from hikari_amd.bands import aligned_bounds, tile_grid, tile_of, tile_reassembly_copies
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tile_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, counts, err = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert err is None, err
+    ny, nx = tile_grid(world)
+    assert (ny, nx) == (2, 2)
+    tiles = [tile_of(k, world, TW, TH, aligned_bounds(ny, TH), [aligned_bounds(nx, TW)] * ny) for k in range(world)]
+    frame = torch.zeros((TH, TW, 8), dtype=torch.uint8)
+    for dst, src in tile_reassembly_copies(frame, torch.from_numpy(gathered), tiles):
+        dst.copy_(src)
+    whole = _tile_render(None)
+    assert np.array_equal(frame.numpy(), whole)
+    assert all(v > 0 for v in counts)
+
+
+@pytest.mark.parametrize("world", [2, 4, 6, 8])
+def test_tiles_partition_and_rebalance(world):
+    """Tile geometry: the tiles of every world size partition the frame, and rebalance_tiles keeps a partition while
+    moving the boundaries towards equal per-tile times."""
+    from hikari_amd.bands import aligned_bounds, rebalance_tiles, tile_grid, tile_of
+    W, H = 3840, 2160
+    ny, nx = tile_grid(world)
+    rb, cb = aligned_bounds(ny, H), [aligned_bounds(nx, W)] * ny
+    for _ in range(2):
+        cover = np.zeros((H, W), np.int32)
+        tiles = [tile_of(k, world, W, H, rb, cb) for k in range(world)]
+        for t in tiles:
+            cover[t.y0: t.y0 + t.rows, t.x0: t.x0 + t.cols] += 1
+        assert (cover == 1).all()
+        times = [1.0 + (t.y0 + t.rows / 2) / H + 0.5 * (t.x0 > 0) for t in tiles]  # costlier lower / right tiles
+        rb, cb = rebalance_tiles(rb, cb, times)
+        assert rb[0] == 0 and rb[-1] == H and all(c[0] == 0 and c[-1] == W for c in cb)

@@ -18,8 +18,11 @@ every rank's band timed, the boundaries moved to equal measured cost, timed agai
 printed beside it.  --overhead-ms X adds the measured per-frame cost of the collective path itself (the
 band copy, the all-gather's stream waits and the reorder at world size 1: HK_BENCH_DIST=1 minus the
 single-GPU line) to every N > 1 frame.
-usage: python tools/band_scaling.py [config] [steps] [--bands] [--kernels] [--only N] [--balance R] [--overhead-ms X]
-                                   [--gather peer|ring] [--opts key=value,...]
+--tiles: 2-D tiles instead of row bands (hk_resize_tile; bands.tile_grid: 2x1 at N = 2, 2x2 at 4, 4x2 at 8), balanced
+with bands.rebalance_tiles (row bands on their slowest tile, the column split inside each row band on its two tiles);
+the per-peer gather then moves the largest tile per link.
+usage: python tools/band_scaling.py [config] [steps] [--bands] [--tiles] [--kernels] [--only N] [--balance R]
+                                   [--overhead-ms X] [--gather peer|ring] [--opts key=value,...]
 --opts: runtime options (hk_set_option) of every band's renderer, for A/B runs."""
 import json
 import sys
@@ -33,7 +36,8 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "bevy-hikari_amd"))
 import bench  # noqa: E402
 from hikari_amd import HikariRenderer, HikariSettings, Upscale, examples, frame_inputs  # noqa: E402
-from hikari_amd.bands import band_of, equal_bounds, halo_rows, rebalance, stripe_gather_rows, use_stripes  # noqa: E402
+from hikari_amd.bands import (aligned_bounds, band_of, equal_bounds, halo_rows, rebalance, rebalance_tiles,  # noqa: E402
+                              stripe_gather_rows, tile_gather_shape, tile_grid, tile_of, use_stripes)
 
 cfg_name = sys.argv[1] if len(sys.argv) > 1 else "cornell-1080p-nee"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 50
@@ -73,8 +77,8 @@ opts = {"gbuffer_reuse": 1 if cfg.get("spp", 1) > 1 else 0,
         **{k: float(v) for k, v in (kv.split("=") for kv in arg("--opts", "").split(",") if kv)}}
 
 
-def rank_ms(n, rank, stripes, bounds):
-    """ms/frame of rank `rank`'s rows of an N-way split, alone on the GPU."""
+def rank_ms(n, rank, stripes, bounds, col_bounds=None):
+    """ms/frame of rank `rank`'s rows (or tile: col_bounds given) of an N-way split, alone on the GPU."""
     if True:
         r = HikariRenderer(0, opts)
         r.set_noise()
@@ -84,6 +88,9 @@ def rank_ms(n, rank, stripes, bounds):
             r.resize(W, H, 1.0)
         elif stripes:
             r.resize_striped(W, H, rank, n)
+        elif col_bounds is not None:
+            t = tile_of(rank, n, W, H, bounds, col_bounds)
+            r.resize_tile(W, H, t.x0, t.cols, t.y0, t.rows)
         else:
             b = band_of(rank, n, H, bounds)
             r.resize(W, H, 1.0, b.y0, b.rows)
@@ -121,8 +128,21 @@ for n in (1, 2, 4, 8):
     if only is not None and n != only:
         continue
     stripes = use_stripes(cfg["spatial"], cfg["denoise"]) and "--bands" not in sys.argv
+    tiles = "--tiles" in sys.argv and not stripes and tile_grid(n)[1] > 1
     if n == 1 or stripes:
         worst = max(rank_ms(n, rank, stripes, None) for rank in sorted({0, n // 2, n - 1}))  # edge and middle
+    elif tiles:
+        ny, nx = tile_grid(n)
+        bounds, cols = aligned_bounds(ny, H), [aligned_bounds(nx, W)] * ny
+        times = [rank_ms(n, k, False, bounds, cols) for k in range(n)]
+        out["equal_bands"][n] = round(max(times), 4)
+        print(f"N={n}: equal {ny}x{nx} tiles {[round(t, 3) for t in times]}", flush=True)
+        for _ in range(rounds):
+            bounds, cols = rebalance_tiles(bounds, cols, times)
+            times = [rank_ms(n, k, False, bounds, cols) for k in range(n)]
+            print(f"N={n}: tiles rows {bounds} cols {cols} -> {[round(t, 3) for t in times]}", flush=True)
+        out["bounds"][n] = {"rows": [int(v) for v in bounds], "cols": [[int(v) for v in c] for c in cols]}
+        worst = max(times)
     else:
         bounds = equal_bounds(n, H)
         times = [rank_ms(n, k, False, bounds) for k in range(n)]
@@ -139,6 +159,9 @@ for n in (1, 2, 4, 8):
         g = allgather_ms(n)
     elif n == 1 or stripes:
         g = peer_gather_ms(n, stripe_gather_rows(n, H)[0] if n > 1 else H)
+    elif tiles:
+        tr, tc = tile_gather_shape(bounds, cols)
+        g = peer_gather_ms(n, tr) * tc / W  # the largest (padded) tile per link
     else:
         g = peer_gather_ms(n, max(b - a for a, b in zip(bounds[:-1], bounds[1:])))
     ov = out["overhead_ms"] if n > 1 else 0.0
