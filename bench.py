@@ -199,6 +199,18 @@ def load_pmc_traffic(config: str, kernel: str):
         return None
 
 
+def load_valu_issue(config: str, kernel: str):
+    """VALU instructions per launch of `kernel` under `config` (rocprofv3 --pmc SQ_INSTS_VALU, every kernel alone) from
+    the committed profiles/valu_issue.json (tools/valu_summary.py), if present."""
+    p = ROOT / "profiles" / "valu_issue.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text())["configs"][config]["kernels"][kernel]["valu_per_launch"]
+    except (KeyError, ValueError):
+        return None
+
+
 def load_traversal_bytes(config: str):
     """Traversal bytes per frame of `config` (nodes, triangles, instances, hit_info of the
     light passes, priced in reference record sizes) from the committed profiles/traversal_bytes.json
@@ -224,6 +236,15 @@ def load_lane_efficiency(config: str, wavefront: bool):
         return {k: v["efficiency"] for k, v in d["wavefront" if wavefront else "megakernel"].items()}
     except (KeyError, ValueError):
         return None
+
+
+def valu_issue(config: str, kernel: str, dur_ms: float):
+    valu = load_valu_issue(config, kernel)
+    if valu is None or not dur_ms:
+        return None
+    floor = valu * 4 / (1024 * 2.4e9) * 1e3
+    return {"valu_per_launch": valu, "issue_floor_ms": round(floor, 4), "valu_frac": round(floor / dur_ms, 4),
+            "clock_ghz": 2.4, "simds": 1024}
 
 
 def json_stdout():
@@ -696,7 +717,12 @@ def main():
                          round(traffic / (dur * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": ref_bytes, "bytes_per_pixel": list(BYTES_PER_PIXEL.get(dom, (0, 0))),
                          "pixels_per_launch": pix, "covered_pixels": int(cov_px), "duration_ms": round(dur, 4),
-                         "duration": "isolated" if isolated else "in frame (overlapped)"},
+                         "duration": "isolated" if isolated else "in frame (overlapped)",
+                         # the bound the traversal kernels actually meet: vector issue.  A wave64 VALU instruction holds
+                         # its SIMD's issue for 4 cycles, so the launch needs valu x 4 / (1024 SIMDs x 2.4 GHz) of issue
+                         # time at least; valu_frac = that floor / the measured duration (profiles/
+                         # valu_issue.json: PMC SQ_INSTS_VALU per launch of this config's kernel alone)
+                         "valu_issue": valu_issue(args.config, dom, dur) if world == 1 else None},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
             # each kernel alone on the GPU (the untimed isolated frames after the timed region)
             "isolated_kernel_ms": None if not isolated else {k: round(v, 4) for k, v in isolated.items()},

@@ -911,8 +911,13 @@ HKD f3 local_to_world_normal(const hk_instance& in, f3 n)
 // of a traverse_top walk adds the wave's active lanes (its first active lane counts for the wave), so
 // sum(active) / (64 x sum(iterations)) is the fraction of SIMD lanes doing walk work, idle lanes of
 // the wave (walks already ended, lanes with no ray) included.
+// Slot 0: the traverse_top walks; slots 1-4: the stages of spatial reuse's neighbour loop (k_spatial: a neighbour
+// tested, a depth-march tap, the record tests, the shade / jacobian / merge), each tick at a stage's entry, so
+// active / (64 x iterations) of a slot is the fraction of the wave's lanes that do that stage's work when it runs.
+constexpr int LANE_SLOTS = 5;
 #ifdef HK_LANE_STATS
-extern __device__ unsigned long long hk_lane_stats_dev[2];
+extern __device__ unsigned long long hk_lane_stats_dev[2 * LANE_SLOTS];
+template <int SLOT = 0>
 struct LaneStats {
     unsigned long long act = 0, its = 0;
     HKD void tick()
@@ -926,16 +931,20 @@ struct LaneStats {
     HKD ~LaneStats()
     {
         if (its) {
-            atomicAdd(&hk_lane_stats_dev[0], act);
-            atomicAdd(&hk_lane_stats_dev[1], its);
+            atomicAdd(&hk_lane_stats_dev[2 * SLOT], act);
+            atomicAdd(&hk_lane_stats_dev[2 * SLOT + 1], its);
         }
     }
 };
-#define HK_LANE_STATS_DECL LaneStats lane_stats_
+#define HK_LANE_STATS_DECL LaneStats<0> lane_stats_
 #define HK_LANE_STATS_TICK lane_stats_.tick()
+#define HK_STAGE_STATS_DECL LaneStats<1> stage1_; LaneStats<2> stage2_; LaneStats<3> stage3_; LaneStats<4> stage4_
+#define HK_STAGE_TICK(k) stage##k##_.tick()
 #else
 #define HK_LANE_STATS_DECL
 #define HK_LANE_STATS_TICK
+#define HK_STAGE_STATS_DECL
+#define HK_STAGE_TICK(k)
 #endif
 
 // Several visits per iteration where the order allows it (walk_step): an inner child-box node p

@@ -22,19 +22,19 @@
 namespace hk {
 
 #ifdef HK_LANE_STATS
-__device__ unsigned long long hk_lane_stats_dev[2];
+__device__ unsigned long long hk_lane_stats_dev[2 * LANE_SLOTS];
 #endif
-// traverse_top lane statistics since the last call (builds with -DHK_LANE_STATS; false otherwise)
-bool lane_stats_take(unsigned long long out[2], hipStream_t st)
+// lane statistics of every slot (LaneStats) since the last call (builds with -DHK_LANE_STATS; false otherwise)
+bool lane_stats_take(unsigned long long out[2 * LANE_SLOTS], hipStream_t st)
 {
 #ifdef HK_LANE_STATS
-    unsigned long long zero[2] = {0, 0};
+    unsigned long long zero[2 * LANE_SLOTS] = {};
     if (hipStreamSynchronize(st) != hipSuccess) return false;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hk_lane_stats_dev), sizeof(zero)) != hipSuccess) return false;
     return hipMemcpyToSymbol(HIP_SYMBOL(hk_lane_stats_dev), zero, sizeof(zero)) == hipSuccess;
 #else
     (void)st;
-    out[0] = out[1] = 0;
+    for (int k = 0; k < 2 * LANE_SLOTS; ++k) out[k] = 0;
     return false;
 #endif
 }
@@ -1753,7 +1753,9 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
     const float srand = sum4(s.random);
     const f3 s_visible = xyz(s.visible_position);
     const f3 s_normal = s.visible_normal;
+    HK_STAGE_STATS_DECL;
     for (uint32_t i = 1u; i <= COUNT; i += 1u) {
+        HK_STAGE_TICK(1);
         float px = HK_TAU * hk_fract(((float)i * HK_GOLDEN_RATIO + srand) + rf);
         const float py = F.sp_py[EMISSIVE_LIT][i - 1u];  // sqrt(i / COUNT) * RANGE
         float sn, cs;
@@ -1792,6 +1794,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         f2 dir = mk2(offset.x * inv_len, offset.y * inv_len);
         const float sx = (float)F.s[0], sy = (float)F.s[1];
         for (uint32_t j = 1u; j <= tap_count; j += 1u) {
+            HK_STAGE_TICK(2);
             float tap_dist = (float)j * tap_interval;
             f2 tuv = mk2(uv.x + div_by(tap_dist * dir.x, sx, F.inv_s[0]), uv.y + div_by(tap_dist * dir.y, sy, F.inv_s[1]));
             int32_t tdx, tdy;
@@ -1814,6 +1817,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
             }
         }
         if (occluded) continue;
+        HK_STAGE_TICK(3);
         // the neighbour's reservoir, its 16-byte planes loaded as the tests need them (the rejection
         // tests read plane 3 (count, normals) and plane 2 (sample position); planes 0-1 only for a
         // neighbour that is merged): the same values as load_res, fewer gathers for rejected ones
@@ -1847,6 +1851,7 @@ HKD void spatial_body(const FrameArgs& A, const ChannelArgs& C, int32_t x, int32
         const float to_sample_length = sqrtf(dot(to_sample, to_sample));
         f3 sample_direction = to_sample * rcp_exact(to_sample_length);
         if (dot(sample_direction, s_normal) < 0.0f) continue;
+        HK_STAGE_TICK(4);
 
         // merge_reservoir(r, q, p / jacobian): the fields of q that the merge reads
         float q_w, q_count, q_rand;

@@ -152,7 +152,7 @@ void launch_smaa(const PostArgs& P, hipStream_t st);
 void launch_smaa_extrapolate(const PostArgs& P, hipStream_t st);
 void launch_taa(const PostArgs& P, hipStream_t st);
 
-bool lane_stats_take(unsigned long long out[2], hipStream_t st);
+bool lane_stats_take(unsigned long long out[2 * LANE_SLOTS], hipStream_t st);
 void launch_gbuffer(const FrameArgs& A, const ViewArgs& V, uint2* albedo, uint32_t stack_need, hipStream_t st);
 void launch_direct_fused(const FrameArgs& A, const ChannelArgs& C0, const ChannelArgs& C1, hipStream_t st);
 void launch_albedo(const FrameArgs& A, uint2* albedo, hipStream_t st);

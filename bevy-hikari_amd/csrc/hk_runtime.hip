@@ -486,18 +486,23 @@ hipEvent_t take_event(hk_ctx* c)
 // Launch wrapper: records HIP events around the kernel on its own stream when timing is on.
 void lane_stats_account(hk_ctx* c, const char* name, hipStream_t st)
 {
-    unsigned long long v[2];
-    if (!lane_stats_take(v, st) || !v[1]) return;
-    size_t k = 0;
-    for (; k < c->lane_names.size(); ++k)
-        if (c->lane_names[k] == name) break;
-    if (k == c->lane_names.size()) {
-        c->lane_names.push_back(name);
-        c->lane_act.push_back(0);
-        c->lane_its.push_back(0);
+    unsigned long long v[2 * LANE_SLOTS];
+    if (!lane_stats_take(v, st)) return;
+    static const char* const stage[LANE_SLOTS] = {"", "/neighbour", "/march_tap", "/record_tests", "/merge"};
+    for (int slot = 0; slot < LANE_SLOTS; ++slot) {
+        if (!v[2 * slot + 1]) continue;
+        const std::string key = std::string(name) + stage[slot];
+        size_t k = 0;
+        for (; k < c->lane_names.size(); ++k)
+            if (c->lane_names[k] == key) break;
+        if (k == c->lane_names.size()) {
+            c->lane_names.push_back(key);
+            c->lane_act.push_back(0);
+            c->lane_its.push_back(0);
+        }
+        c->lane_act[k] += v[2 * slot];
+        c->lane_its[k] += v[2 * slot + 1];
     }
-    c->lane_act[k] += v[0];
-    c->lane_its[k] += v[1];
 }
 
 template <typename F>
@@ -506,7 +511,7 @@ void timed(hk_ctx* c, const char* name, hipStream_t st, F&& launch)
 #ifdef HK_LANE_STATS
     // instrumented build: attribute the walk statistics to this launch (serialises the streams)
     (void)hipDeviceSynchronize();
-    unsigned long long drop[2];
+    unsigned long long drop[2 * LANE_SLOTS];
     (void)lane_stats_take(drop, st);
     launch();
     lane_stats_account(c, name, st);
