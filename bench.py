@@ -242,8 +242,8 @@ def valu_issue(config: str, kernel: str, dur_ms: float):
     valu = load_valu_issue(config, kernel)
     if valu is None or not dur_ms:
         return None
-    floor = valu * 4 / (1024 * 2.4e9) * 1e3
-    return {"valu_per_launch": valu, "issue_floor_ms": round(floor, 4), "valu_frac": round(floor / dur_ms, 4),
+    floor = valu * 2 / (1024 * 2.4e9) * 1e3
+    return {"valu_per_launch": valu, "alu_floor_ms": round(floor, 4), "valu_frac": round(floor / dur_ms, 4),
             "clock_ghz": 2.4, "simds": 1024}
 
 
@@ -319,43 +319,15 @@ def main():
     r.set_wavefront(wavefront)
     bounds, balance = None, []
     # 2-D tiles (north_star: "frames tile-partition across the 8 GPUs"; bands.tile_grid: 2x2 at N = 4, 4x2 at N = 8)
-    # for the frames with neighbour reads at 4 or more ranks, HK_BENCH_DECOMP=bands keeps row bands
-    tiles = dist_on and not stripes and tile_grid(world)[1] > 1 and os.environ.get("HK_BENCH_DECOMP", "tiles") == "tiles"
+    # for the frames with neighbour reads with HK_BENCH_DECOMP=tiles.  Default: cost-balanced row bands, which measured
+    # faster on the bench scenes (their cost sits in the middle rows, and N balanced bands follow it more closely than
+    # N / 2 balanced row bands of 2 tiles: scene N = 4 0.609 vs 0.661 ms, N = 8 0.448 vs 0.498; city N = 8 0.795 vs
+    # 0.804; profiles/r06/c7, c8)
+    tiles = dist_on and not stripes and tile_grid(world)[1] > 1 and os.environ.get("HK_BENCH_DECOMP", "bands") == "tiles"
     col_bounds, my_tile, all_tiles = None, None, None
     if stripes:
         r.resize_striped(W, H, rank, world)
         band, gather_index = stripe_gather_rows(world, H)  # padded rows per rank
-    elif dist_on:
-        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 5) of a short
-        # calibration on the current bands — frames 0..5 rendered, 3..5 timed per rank, the times all-gathered
-        # — each moving the boundaries to equal measured cost.  Then every rank starts the run from frame 0
-        # on its final band (hk_resize zero-fills the reservoirs, as at the start of any run).
-        bounds = equal_bounds(world, H)
-        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "5")) if world > 1 else 0):
-            b = band_of(rank, world, H, bounds)
-            r.resize(W, H, 1.0, b.y0, b.rows)
-            for f in range(6):
-                if f == 3:
-                    torch.cuda.synchronize()
-                    t_cal = time.perf_counter()
-                fi = frame_inputs(f, cam, lights, W, H)
-                r.render_gbuffer(fi)
-                r.render_frame(s, fi)
-                if st.denoise:
-                    r.denoise(s, fi)
-                r.tone_sum(s)
-            r.sync()
-            torch.cuda.synchronize()
-            t_cal = torch.tensor([(time.perf_counter() - t_cal) / 3.0], dtype=torch.float64,
-                                 device="cpu" if rehearsal else "cuda")
-            times = torch.zeros(world, dtype=torch.float64, device=t_cal.device)
-            dist.all_gather_into_tensor(times, t_cal)
-            times = times.cpu().numpy()
-            balance.append({"bounds": list(bounds), "ms": [round(float(t) * 1e3, 4) for t in times]})
-            bounds = rebalance(bounds, times)
-        b = band_of(rank, world, H, bounds)
-        r.resize(W, H, 1.0, b.y0, b.rows)
-        band, gather_index = band_gather_rows(bounds)
     elif tiles:
         # cost-balanced tiles (bands.rebalance_tiles): the same calibration as the bands, each rank timing its tile
         ny, nx = tile_grid(world)
@@ -388,6 +360,37 @@ def main():
         r.resize_tile(W, H, my_tile.x0, my_tile.cols, my_tile.y0, my_tile.rows)
         tile_rows, tile_cols = tile_gather_shape(bounds, col_bounds)
         band = tile_rows
+    elif dist_on:
+        # cost-balanced row bands (bands.rebalance): HK_BENCH_BALANCE rounds (default 5) of a short
+        # calibration on the current bands — frames 0..5 rendered, 3..5 timed per rank, the times all-gathered
+        # — each moving the boundaries to equal measured cost.  Then every rank starts the run from frame 0
+        # on its final band (hk_resize zero-fills the reservoirs, as at the start of any run).
+        bounds = equal_bounds(world, H)
+        for _ in range(int(os.environ.get("HK_BENCH_BALANCE", "5")) if world > 1 else 0):
+            b = band_of(rank, world, H, bounds)
+            r.resize(W, H, 1.0, b.y0, b.rows)
+            for f in range(6):
+                if f == 3:
+                    torch.cuda.synchronize()
+                    t_cal = time.perf_counter()
+                fi = frame_inputs(f, cam, lights, W, H)
+                r.render_gbuffer(fi)
+                r.render_frame(s, fi)
+                if st.denoise:
+                    r.denoise(s, fi)
+                r.tone_sum(s)
+            r.sync()
+            torch.cuda.synchronize()
+            t_cal = torch.tensor([(time.perf_counter() - t_cal) / 3.0], dtype=torch.float64,
+                                 device="cpu" if rehearsal else "cuda")
+            times = torch.zeros(world, dtype=torch.float64, device=t_cal.device)
+            dist.all_gather_into_tensor(times, t_cal)
+            times = times.cpu().numpy()
+            balance.append({"bounds": list(bounds), "ms": [round(float(t) * 1e3, 4) for t in times]})
+            bounds = rebalance(bounds, times)
+        b = band_of(rank, world, H, bounds)
+        r.resize(W, H, 1.0, b.y0, b.rows)
+        band, gather_index = band_gather_rows(bounds)
     else:
         band = H
         r.resize(W, H, 1.0)
@@ -429,7 +432,7 @@ def main():
     pending = [None, None]
     if reorder:  # stripes / uneven bands back in frame order, on a side stream after each gather
         frame_t = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(2)]
-        index_t = torch.from_numpy(gather_index).to("cuda")
+        index_t = None if tiles else torch.from_numpy(gather_index).to("cuda")
 
         # one strided row copy per rank (bands.reassembly_copies); torch.index_select over the frame's row
         # indices took ~0.1 ms per 1080p frame (per-element index arithmetic), the row copies a few microseconds
@@ -536,7 +539,7 @@ def main():
                 return
             if rehearsal:
                 if peer_stripes:
-                    host = torch.empty((world * band, W, 4), dtype=torch.float16)
+                    host = torch.empty((world * band, part_w, 4), dtype=torch.float16)
                     wait_all(peer_gather(host, band_t[k].cpu(), rank, world))
                     full_t[k].copy_(host)
                 else:
@@ -718,10 +721,10 @@ def main():
                          "bytes_per_launch": ref_bytes, "bytes_per_pixel": list(BYTES_PER_PIXEL.get(dom, (0, 0))),
                          "pixels_per_launch": pix, "covered_pixels": int(cov_px), "duration_ms": round(dur, 4),
                          "duration": "isolated" if isolated else "in frame (overlapped)",
-                         # the bound the traversal kernels actually meet: vector issue.  A wave64 VALU instruction holds
-                         # its SIMD's issue for 4 cycles, so the launch needs valu x 4 / (1024 SIMDs x 2.4 GHz) of issue
-                         # time at least; valu_frac = that floor / the measured duration (profiles/
-                         # valu_issue.json: PMC SQ_INSTS_VALU per launch of this config's kernel alone)
+                         # the traversal kernels' other bound: vector issue.  A wave64 VALU instruction holds its SIMD's
+                         # 32-lane ALU for 2 cycles (one wave alone issues one per 4), so the launch needs at least
+                         # valu x 2 / (1024 SIMDs x 2.4 GHz) of ALU time; valu_frac = that floor / the measured duration
+                         # (profiles/valu_issue.json: PMC SQ_INSTS_VALU per launch of the kernel alone)
                          "valu_issue": valu_issue(args.config, dom, dur) if world == 1 else None},
             "kernel_ms": {k: round(v, 4) for k, v in timing.items()},
             # each kernel alone on the GPU (the untimed isolated frames after the timed region)

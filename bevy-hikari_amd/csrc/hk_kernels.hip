@@ -2346,6 +2346,8 @@ __global__ __launch_bounds__(256) void k_trace(Scene sc, const float* rays, cons
 
 // ------------------------------------------------------------------ launchers
 static dim3 tiles(uint32_t width, int32_t rows) { return dim3((width + 15u) / 16u, ((uint32_t)rows + 15u) / 16u, 1); }
+// the pixels of the context's planes a launch-shape choice weighs: the band's rows, at a tile's window width
+static double plane_px(const Frame& F) { return (double)(F.win_cols > 0 ? (uint32_t)F.win_cols : F.s[0]) * (double)F.s_rows; }
 // the tile grid of a launch: its window's rows (Frame::win_rows), else the plane's
 static dim3 tiles(const Frame& F, uint32_t width, int32_t rows)
 {
@@ -2412,7 +2414,7 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
     // staged since round 4 (stage_scene) on frames of >= direct_w4_min_px pixels: cornell 1080p under an orbiting
     // camera direct_lit 0.110 -> 0.098 ms, emissive 0.124 -> 0.109 ms, frame 0.457 -> 0.413 ms (profiles/r04/c22,
     // c23); a 256x256 frame (256 workgroups) lost 3 % with it (c23)
-    const bool big = (double)A.F.s[0] * (double)A.F.s_rows >= A.opt.direct_w4_min_px;
+    const bool big = plane_px(A.F) >= A.opt.direct_w4_min_px;
     const uint32_t lds = lds_plan_bytes(A, PLAN_LIGHT, big);
     if (emissive_lit) {
         const bool val = validation_frame(A.F.number, A.F.emissive_validate_interval);
@@ -2420,7 +2422,7 @@ void launch_direct(const FrameArgs& A, const ChannelArgs& C, bool emissive_lit, 
         else launch_direct_v<true, false, false>(A, C, val, g, 0, st);
     } else {
         const bool val = validation_frame(A.F.number, A.F.direct_validate_interval);
-        if ((double)A.F.s[0] * (double)A.F.s_rows >= A.opt.direct_w4_min_px) {
+        if (plane_px(A.F) >= A.opt.direct_w4_min_px) {
             if (lds) {
                 if (val) hipLaunchKernelGGL((k_direct_lit_w4<true, true>), g, dim3(256), lds, st, A, C);
                 else hipLaunchKernelGGL((k_direct_lit_w4<true, false>), g, dim3(256), lds, st, A, C);

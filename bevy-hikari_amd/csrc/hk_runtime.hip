@@ -364,9 +364,17 @@ int tail_end(hk_ctx* c)
 // long G-buffer and tail to hide, and pipelines at every size: scene 1080p 2-way band 1.12 -> 0.92 ms,
 // 8-way 0.50 -> 0.45, city 4K 8-way 0.90 -> 0.86 (profiles/r05/c21).  Only the schedule changes, never
 // the results.
+// (the pixels of the band's rows, at a 2-D tile's columns + halo: the work its launches cover)
+double ctx_px(const hk_ctx* c)
+{
+    double cols = (double)c->s[0];
+    if (c->core_cols > 0 && c->core_cols < (int32_t)c->S[0])
+        cols = (double)(std::min((int32_t)c->s[0], c->core_col0 + c->core_cols + c->halo) - std::max(0, c->core_col0 - c->halo));
+    return cols * (double)c->s_rows;
+}
 bool pipeline_size(const hk_ctx* c)
 {
-    const double px = (double)c->s[0] * (double)c->s_rows;
+    const double px = ctx_px(c);
     return px >= c->opt[OPT_PIPELINE_MIN_PX] || (c->heavy && px >= c->opt[OPT_PIPELINE_HEAVY_MIN_PX]);
 }
 bool dn_pipeline_enabled(const hk_ctx* c) { return c->on(OPT_TAIL_PIPELINE) && pipeline_size(c); }
@@ -1787,7 +1795,7 @@ int hk_render_frame(hk_ctx* c, const hk_settings* settings, const hk_frame_input
     // tail (cornell 1080p 0.652 -> 0.622 ms); on a small band (a 4- or 8-way split) the two passes
     // on their own overlap the indirect chain better (0.143 vs 0.151 ms).  Options fuse, fuse_min_px.
     const bool fuse = c->albedo_fresh && c->velocity_zero && c->ratio == 1.0f &&
-                      (double)c->s[0] * (double)c->s_rows >= c->opt[OPT_FUSE_MIN_PX] && c->on(OPT_FUSE);
+                      ctx_px(c) >= c->opt[OPT_FUSE_MIN_PX] && c->on(OPT_FUSE);
     // background elision (bg_mask, hk_kernels.hip bg_elide); the separate launches share the pair's mask
     // (direct_pass).  A background pixel's own targets (temporal record, render, variance) are written by
     // that pixel alone, so they elide with or without motion.  Under motion the temporal passes also scatter
