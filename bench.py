@@ -140,7 +140,8 @@ CONFIGS = {
     # one all-gather per displayed frame
     "city-4k-16spp": dict(scene="city", width=3840, height=2160, spatial=True, denoise=True, spp=16, wavefront=True,
                           workload="examples/city.rs layout (City proxy houses) 3840x2160 16spp accumulation "
-                                   "(16 sub-frames per displayed frame), wavefront material-sorted indirect "
+                                   "(16 sub-frames per displayed frame; static camera: the G-buffer traced once per "
+                                   "displayed frame, gbuffer_reuse), wavefront material-sorted indirect "
                                    "shading, row bands + RCCL all-gather"),
 }
 

@@ -12,6 +12,11 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 $OUT/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 timeout -k 10 300 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
+# the driver's own command (BENCH_rNN.json: --gpus 1 --steps 20 --warmup 5) beside the default 100 / 16 (VERDICT r05
+# item 3): its 20 frames are frames 5-24, heavier than the steady state (ReSTIR history filling)
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver_$i.json 2> $OUT/bench_driver_$i.err
+done
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
    -d $R/$OUT/stats -o run -- python $R/bench.py --steps 20 --warmup 3 --cpu-budget 0 > $R/$OUT/stats.log 2>&1)
 # the same with every kernel alone (channel fork and frame pipelining off): the isolated durations of the roofline

@@ -21,9 +21,10 @@ else
     cornell-orbit:cornell-1080p-nee-orbit city-orbit:city-4k-orbit
   BENCH_ARGS='--steps 2 --warmup 1 --cpu-budget 0' bash tools/gpu_run.sh $TAG '' \
     city16-wavefront:city-4k-16spp city16-megakernel:city-4k-16spp:HK_BENCH_WAVEFRONT=0
-  timeout -k 10 300 python tools/band_scaling.py cornell-1080p-nee 50 --overhead-ms 0.003 > gpurun_out/$TAG/bands_cornell.log 2>&1
-  timeout -k 10 400 python tools/band_scaling.py scene-1080p-full 30 --overhead-ms 0.008 > gpurun_out/$TAG/bands_scene.log 2>&1
-  timeout -k 10 600 python tools/band_scaling.py city-4k 30 --overhead-ms 0.044 > gpurun_out/$TAG/bands_city-4k.log 2>&1
+  # overheads: the world-1 collective path with the per-peer exchange's RCCL self send / receive (profiles/r06/c3)
+  timeout -k 10 300 python tools/band_scaling.py cornell-1080p-nee 50 --overhead-ms 0.012 > gpurun_out/$TAG/bands_cornell.log 2>&1
+  timeout -k 10 400 python tools/band_scaling.py scene-1080p-full 30 --overhead-ms 0.014 > gpurun_out/$TAG/bands_scene.log 2>&1
+  timeout -k 10 600 python tools/band_scaling.py city-4k 30 --overhead-ms 0.057 > gpurun_out/$TAG/bands_city-4k.log 2>&1
   for f in gpurun_out/$TAG/bands_*.log; do tail -n 2 $f; done
   echo round-final-b-done
 fi
