@@ -1596,6 +1596,18 @@ HKD float compute_jacobian(const Sample& q, const Sample& r)
 }
 
 // blue noise (light.wgsl:1075-1079): nearest + repeat => texel ((x + n) & 63, (y + n) & 63)
+HKD uchar4 noise_texel(const uchar4* noise, uint32_t number, int32_t x, int32_t y)
+{
+    uint32_t id = number & 15u;
+    uint32_t tx = ((uint32_t)x + number) & 63u, ty = ((uint32_t)y + number) & 63u;
+    return noise[(id * 64u + ty) * 64u + tx];
+}
+HKD f4 noise_of(uchar4 t, uint32_t number)
+{
+    float fn = (float)number * HK_GOLDEN_RATIO;
+    return mk4(hk_fract(hk_unorm8_fast(t.x) + fn), hk_fract(hk_unorm8_fast(t.y) + fn), hk_fract(hk_unorm8_fast(t.z) + fn),
+               hk_fract(hk_unorm8_fast(t.w) + fn));
+}
 HKD f4 noise_random(const uchar4* noise, uint32_t number, int32_t x, int32_t y)
 {
     uint32_t id = number & 15u;

@@ -282,6 +282,55 @@ struct DirectPixel {
     f3 normal;
     f2 imf;
 };
+// A light pass's G-buffer texels and blue-noise texel for its pixel, loaded at the kernel's start, before the
+// workgroup's scene staging: their latency then overlaps the staging copy instead of following its barrier (the
+// loads the pass makes anyway — load_position / load_normal / load_instance_material / load_velocity_uv at the
+// jittered coordinates, noise_random's texel — so the values are the same; a background pixel reads them too).
+struct PixelTexels {
+    float4 pd, vel;
+    float2 imf;
+    uint32_t normal;
+    uchar4 noise;
+};
+HKD PixelTexels load_pixel_texels(const FrameArgs& A, int32_t x, int32_t y)
+{
+    const Frame& F = A.F;
+    PixelTexels t;
+    int32_t dx, dy;
+    jittered_coords(F, coords_to_uv(x, y, F.s), dx, dy);
+    if (in_frame(dx, dy, F.S)) {
+        const int32_t i = band_index(F, dx, dy, F.S[0], F.S_row0, F.S_rows);
+        t.pd = A.G.position[i];
+        t.vel = A.G.velocity_uv[i];
+        t.imf = A.G.instance_material[i];
+        t.normal = A.G.normal[i];
+    } else {
+        t.pd = t.vel = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        t.imf = make_float2(0.0f, 0.0f);
+        t.normal = 0u;
+    }
+    t.noise = noise_texel(A.noise, F.number, x, y);
+    return t;
+}
+HKD f3 texel_normal(uint32_t n) { return mk3(hk_unpack_snorm8_fast(n, 0), hk_unpack_snorm8_fast(n, 1), hk_unpack_snorm8_fast(n, 2)); }
+HKD DirectPixel direct_pixel_of(const FrameArgs& A, int32_t x, int32_t y, const PixelTexels& t)
+{
+    const Frame& F = A.F;
+    DirectPixel p;
+    p.idx = s_index(F, x, y);
+    p.uv = coords_to_uv(x, y, F.s);
+    p.pd = mk4(t.pd.x, t.pd.y, t.pd.z, t.pd.w);
+    p.normal = mk3(0, 0, 0);
+    p.imf = mk2(0, 0);
+    p.velocity_uv = p.random = mk4(0, 0, 0, 0);
+    if (p.pd.w >= HK_F32_EPSILON) {
+        p.normal = texel_normal(t.normal);
+        p.imf = mk2(t.imf.x, t.imf.y);
+        p.velocity_uv = mk4(t.vel.x, t.vel.y, t.vel.z, t.vel.w);
+        p.random = noise_of(t.noise, F.number);
+    }
+    return p;
+}
 HKD DirectPixel load_direct_pixel(const FrameArgs& A, int32_t x, int32_t y)
 {
     const Frame& F = A.F;
@@ -699,13 +748,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 template <bool LDS, bool VD, bool VE>
 __global__ __launch_bounds__(256) void k_direct_fused(FrameArgs A, ChannelArgs C0, ChannelArgs C1)
 {
+    int32_t x, y;
+    const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    PixelTexels tex;
+    if (active) tex = load_pixel_texels(A, x, y);  // in flight during the staging
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
-    int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
-        const DirectPixel P = load_direct_pixel(A, x, y);
+    if (active) {
+        const DirectPixel P = direct_pixel_of(A, x, y, tex);
         const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
         if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
             const Reservoir z = background_reservoir();
@@ -732,13 +784,16 @@ template <bool LDS, bool VD, bool VE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_fused_w4(FrameArgs A, ChannelArgs C0,
                                                                                                    ChannelArgs C1)
 {
+    int32_t x, y;
+    const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    PixelTexels tex;
+    if (active) tex = load_pixel_texels(A, x, y);  // in flight during the staging
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
-    int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y)) {
-        const DirectPixel P = load_direct_pixel(A, x, y);
+    if (active) {
+        const DirectPixel P = direct_pixel_of(A, x, y, tex);
         const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
         if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
             const Reservoir z = background_reservoir();
@@ -1092,7 +1147,7 @@ struct IndirectState {
 template <bool MULTI, int STAGE = IND_ALL>
 HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
                         uint32_t& n_emitter, const WfArgs* W, uint32_t* key, IndirectState& I, bool& ret,
-                        IndStash* stash = nullptr)
+                        IndStash* stash = nullptr, const PixelTexels* tex = nullptr)
 {
     static_assert(!MULTI || STAGE == IND_ALL, "the wavefront stages cover one bounce");
     I.shadow = false;
@@ -1102,7 +1157,7 @@ HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& 
     const f2 uv = coords_to_uv(x, y, F.s);
     int32_t dx, dy;
     jittered_coords(F, uv, dx, dy);
-    f4 pd = load_position(F, A.G, dx, dy);
+    f4 pd = tex ? mk4(tex->pd.x, tex->pd.y, tex->pd.z, tex->pd.w) : load_position(F, A.G, dx, dy);
     f4 position = mk4(pd.x, pd.y, pd.z, 1.0f);
     float depth = pd.w;
     Sample s = zero_sample();
@@ -1128,12 +1183,12 @@ HKD bool indirect_begin(const FrameArgs& A, const Scene& sc, const ChannelArgs& 
         ret = true;
         return false;
     }
-    f3 normal = normalize(load_normal(F, A.G, dx, dy));
-    f2 imf = load_instance_material(F, A.G, dx, dy);
+    f3 normal = normalize(tex ? texel_normal(tex->normal) : load_normal(F, A.G, dx, dy));
+    f2 imf = tex ? mk2(tex->imf.x, tex->imf.y) : load_instance_material(F, A.G, dx, dy);
     uint32_t im_x = f2u32(imf.x), im_y = f2u32(imf.y);
-    f4 velocity_uv = load_velocity_uv(F, A.G, dx, dy);
+    f4 velocity_uv = tex ? mk4(tex->vel.x, tex->vel.y, tex->vel.z, tex->vel.w) : load_velocity_uv(F, A.G, dx, dy);
 
-    s.random = noise_random(A.noise, F.number, x, y);
+    s.random = tex ? noise_of(tex->noise, F.number) : noise_random(A.noise, F.number, x, y);
     s.visible_position = mk4(position.x, position.y, position.z, depth);
     s.visible_normal = normal;
     s.visible_instance = im_x;
@@ -1337,11 +1392,12 @@ HKD void indirect_end(const FrameArgs& A, const Scene& sc, const ChannelArgs& C,
 // returns (IND_GEN) whether the pixel traces a bounce; (IND_TRACE) the hit's material bin in *key
 template <bool MULTI, int STAGE = IND_ALL>
 HKD bool indirect_body(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
-                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr, IndStash* stash = nullptr)
+                       uint32_t& n_emitter, const WfArgs* W = nullptr, uint32_t* key = nullptr, IndStash* stash = nullptr,
+                       const PixelTexels* tex = nullptr)
 {
     IndirectState I;
     bool ret;
-    if (!indirect_begin<MULTI, STAGE>(A, sc, C, x, y, n_top, n_emitter, W, key, I, ret, stash)) return ret;
+    if (!indirect_begin<MULTI, STAGE>(A, sc, C, x, y, n_top, n_emitter, W, key, I, ret, stash, tex)) return ret;
     Hit sh;
     if (!MULTI && I.shadow)
         sh = traverse_top(sc, I.B.ray, I.B.cand.max_distance, I.B.cand.min_distance, I.B.cand.emissive_instance);
@@ -1355,6 +1411,13 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
     const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    // The multi-light variant loads its pixel's texels before the staging (city 4K 0.536 -> 0.497 ms, scene 0.251 ->
+    // 0.243, profiles/r06/c13).  The one-light variant does not: the texels live across the staging took it 92 -> 99
+    // VGPRs, 5 -> 4 waves per SIMD (cornell 0.178 -> 0.192 ms), and the position + noise texels alone (95 VGPRs)
+    // measured 0.181.
+    constexpr bool PRE = MULTI && !CS;
+    PixelTexels tex;
+    if (PRE && active) tex = load_pixel_texels(A, x, y);  // in flight during the staging
     Scene sc = A.sc;
     if constexpr (LDS) {
         sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
@@ -1372,7 +1435,7 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
         // the pixel's fields through the walks in LDS (IndStash): k_indirect alone city 4K 0.590 -> 0.558 ms, scene
         // 1080p 0.268 -> 0.259, cornell 1080p 0.180 -> 0.179 (17 KiB per workgroup; still 5 waves per SIMD)
         __shared__ IndStash stash;
-        indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter, nullptr, nullptr, &stash);
+        indirect_body<MULTI>(A, sc, C, x, y, n_top, n_emitter, nullptr, nullptr, &stash, PRE ? &tex : nullptr);
     }
     if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
