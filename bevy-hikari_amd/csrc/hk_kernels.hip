@@ -282,10 +282,12 @@ struct DirectPixel {
     f3 normal;
     f2 imf;
 };
-// A light pass's G-buffer texels and blue-noise texel for its pixel, loaded at the kernel's start, before the
-// workgroup's scene staging: their latency then overlaps the staging copy instead of following its barrier (the
-// loads the pass makes anyway — load_position / load_normal / load_instance_material / load_velocity_uv at the
-// jittered coordinates, noise_random's texel — so the values are the same; a background pixel reads them too).
+// A light pass's G-buffer texels and blue-noise texel for its pixel, loaded together at the kernel's start: before
+// the workgroup's scene staging, their latency overlaps the staging copy instead of following its barrier; without
+// staging, they are one round trip instead of the position's followed by the rest once the pixel is known to be
+// covered.  The loads the pass makes anyway (load_position / load_normal / load_instance_material /
+// load_velocity_uv at the jittered coordinates, noise_random's texel), so the values are the same; a background
+// pixel reads them too.
 struct PixelTexels {
     float4 pd, vel;
     float2 imf;
@@ -1411,13 +1413,14 @@ __global__ __launch_bounds__(256) void k_indirect(FrameArgs A, ChannelArgs C)
 {
     int32_t x, y;
     const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
-    // The multi-light variant loads its pixel's texels before the staging (city 4K 0.536 -> 0.497 ms, scene 0.251 ->
-    // 0.243, profiles/r06/c13).  The one-light variant does not: the texels live across the staging took it 92 -> 99
-    // VGPRs, 5 -> 4 waves per SIMD (cornell 0.178 -> 0.192 ms), and the position + noise texels alone (95 VGPRs)
-    // measured 0.181.
-    constexpr bool PRE = MULTI && !CS;
+    // The one-bounce variant without LDS staging (scene, city) loads all of its pixel's texels up front: one round
+    // trip instead of the position's followed by the rest once the pixel is known to be covered (city 4K 0.536 ->
+    // 0.497 ms, scene 0.251 -> 0.243, profiles/r06/c13).  The staged variant (cornell) does not: the texels live
+    // across the staging took it 92 -> 99 VGPRs, 5 -> 4 waves per SIMD (0.178 -> 0.192 ms), and the position + noise
+    // texels alone (95 VGPRs) measured 0.181.  The multi-bounce variants (no BASELINE config) keep their own loads.
+    constexpr bool PRE = !MULTI && !LDS && !CS;
     PixelTexels tex;
-    if (PRE && active) tex = load_pixel_texels(A, x, y);  // in flight during the staging
+    if (PRE && active) tex = load_pixel_texels(A, x, y);
     Scene sc = A.sc;
     if constexpr (LDS) {
         sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
