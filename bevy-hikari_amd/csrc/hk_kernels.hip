@@ -688,9 +688,9 @@ HKD Reservoir background_reservoir()
 // from the same G-buffer texel, so they agree on which pixels are background.
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool VALIDATE>
 HKD void direct_pass(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, int32_t x, int32_t y, uint32_t& n_top,
-                     uint32_t& n_emitter)
+                     uint32_t& n_emitter, const PixelTexels* tex = nullptr)
 {
-    const DirectPixel P = load_direct_pixel(A, x, y);
+    const DirectPixel P = tex ? direct_pixel_of(A, x, y, *tex) : load_direct_pixel(A, x, y);
     const bool background = P.pd.w < HK_F32_EPSILON;
     if constexpr (!EMISSIVE_LIT) {
         if (C.bg && background && (C.bg[P.idx] & (C.bg_need & 15u)) == (C.bg_need & 15u)) return;
@@ -710,13 +710,15 @@ HKD void direct_pass(const FrameArgs& A, const Scene& sc, const ChannelArgs& C, 
 template <bool EMISSIVE_LIT, bool RENDER_EMISSIVE, bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
 {
+    int32_t x, y;
+    const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    PixelTexels tex;
+    if (active) tex = load_pixel_texels(A, x, y);
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
-    int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_pass<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
+    if (active) direct_pass<EMISSIVE_LIT, RENDER_EMISSIVE, VALIDATE>(A, sc, C, x, y, n_top, n_emitter, &tex);
     if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -730,13 +732,15 @@ __global__ __launch_bounds__(256) void k_direct(FrameArgs A, ChannelArgs C)
 template <bool LDS, bool VALIDATE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_direct_lit_w4(FrameArgs A, ChannelArgs C)
 {
+    int32_t x, y;
+    const bool active = tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y);
+    PixelTexels tex;
+    if (active) tex = load_pixel_texels(A, x, y);
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
-    int32_t x, y;
     uint32_t n_top = 0, n_emitter = 0;
-    if (tile_pixel<TRACE_ORDER>(A.F, A.F.s[0], A.F.s_row0, A.F.s_rows, x, y))
-        direct_pass<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter);
+    if (active) direct_pass<false, true, VALIDATE>(A, sc, C, x, y, n_top, n_emitter, &tex);
     if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     wave_count(A.cnt.top, n_top);
     wave_count(A.cnt.emitter, n_emitter);
@@ -986,7 +990,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     DirectPixel P;
     uint32_t bg = BG_SKIP_ALL;
     if (on) {
-        P = load_direct_pixel(A, x, y);
+        P = direct_pixel_of(A, x, y, load_pixel_texels(A, x, y));
         bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
         if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
             const Reservoir z = background_reservoir();
@@ -1534,6 +1538,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         if (active) indirect_body<false>(A, sc, C2, x, y, n_top, n_emitter, nullptr, nullptr, stash);
     } else if (active) {
         const Scene& sc = A.sc;
+        // (its own loads: the texel preload here measured 0-1 % slower on the cornell 2- to 8-way stripes, r06/c16-c17)
         const DirectPixel P = load_direct_pixel(A, x, y);
         const uint32_t bg = bg_elide(C0, P.idx, P.pd.w < HK_F32_EPSILON);
         if (bg == BG_SKIP_OWN) {  // the emissive pass's stores into the spatial pair (direct_body)
