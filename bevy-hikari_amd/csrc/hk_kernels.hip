@@ -2135,6 +2135,35 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
     const Frame& F = A.F;
     int32_t x0, y0;
     tile_origin<XCD_RASTER>(F, F.s_row0, x0, y0);
+    // the pixel's own texels first (its deferred texel at the nearest texel of the jittered uv, albedo, the channels'
+    // render texels), so that their latency overlaps the variance staging instead of following its barrier
+    int32_t x, y;
+    const bool active = tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y);
+    int32_t idx = 0;
+    f2 uv = mk2(0, 0);
+    uint32_t n_bits = 0u;
+    float depth = 0.0f, inst = 0.0f;
+    float2 grad = make_float2(0.0f, 0.0f);
+    uint2 alb = make_uint2(0u, 0u), rtex[C];
+    if (active) {
+        idx = s_index(F, x, y);
+        uv = coords_to_uv(x, y, F.s);
+        f2 duv = jittered_uv(F, uv, 0.5f);
+        int32_t ax, ay, rx, ry;
+        nearest_texel(duv, F.S, ax, ay);
+        // (ax, ay) is a nearest_texel: inside the frame, so the load_* bounds tests always pass; the texels are read
+        // directly, without their branch regions, so all of them are in flight together (same texels, same values)
+        const int32_t g = band_index(F, ax, ay, F.S[0], F.S_row0, F.S_rows);
+        n_bits = A.G.normal[g];
+        depth = A.G.position[g].w;
+        grad = A.G.depth_gradient[g];
+        inst = A.G.instance_material[g].x;
+        alb = D.albedo[g];  // load_albedo(ax, ay): the same band index
+        nearest_texel(uv, F.s, rx, ry);
+        const int32_t ridx = s_index(F, rx, ry);
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) rtex[ch] = D.render[ch][ridx];
+    }
     for (int32_t k = (int32_t)threadIdx.x; k < RW * RW; k += 256) {
         const int32_t ry = k / RW, rx = k - ry * RW;
         const int32_t vidx = rb_index(F, min(max(x0 - 1 + rx, 0), (int32_t)F.s[0] - 1), min(max(y0 - 1 + ry, 0), (int32_t)F.s[1] - 1));
@@ -2142,33 +2171,18 @@ __global__ __launch_bounds__(256) void k_demod3(FrameArgs A, DenoiseArgs D)
         for (int ch = 0; ch < C; ++ch) s_var[ch][ry * RS + rx] = D.variance[ch][vidx];
     }
     __syncthreads();
-    int32_t x, y;
-    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
-    const int32_t idx = s_index(F, x, y);
-    f2 uv = coords_to_uv(x, y, F.s);
-    f2 duv = jittered_uv(F, uv, 0.5f);
-    int32_t ax, ay, rx, ry;
-    nearest_texel(duv, F.S, ax, ay);
-    // (ax, ay) is a nearest_texel: inside the frame, so the load_* bounds tests always pass; the texels are read
-    // directly, without their branch regions, so all of them are in flight together (same texels, same values)
-    float inst;
-    float2 grad;
+    if (!active) return;
     {
-        const int32_t g = band_index(F, ax, ay, F.S[0], F.S_row0, F.S_rows);
-        const uint32_t n = A.G.normal[g];
+        const uint32_t n = n_bits;
         const f3 normal = normalize(mk3(hk_unpack_snorm8_fast(n, 0), hk_unpack_snorm8_fast(n, 1), hk_unpack_snorm8_fast(n, 2)));
-        D.nd[idx] = make_float4(normal.x, normal.y, normal.z, A.G.position[g].w);  // denoise.wgsl:220-223, 197-200
-        grad = A.G.depth_gradient[g];
-        inst = A.G.instance_material[g].x;
+        D.nd[idx] = make_float4(normal.x, normal.y, normal.z, depth);  // denoise.wgsl:220-223, 197-200
     }
-    f3 albedo = xyz(load_albedo(F, D.albedo, ax, ay));
-    nearest_texel(uv, F.s, rx, ry);
-    const int32_t ridx = s_index(F, rx, ry);
+    f3 albedo = mk3(unpack_lo16float(alb.x), unpack_hi16float(alb.x), unpack_lo16float(alb.y));
     f3 out[3] = {mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0)};
     float den[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) {
-        f3 irr = xyz(load_rgba16f(D.render[ch], ridx));
+        f3 irr = mk3(unpack_lo16float(rtex[ch].x), unpack_hi16float(rtex[ch].x), unpack_lo16float(rtex[ch].y));
         out[ch] = mk3(albedo.x < 0.01f ? 0.0f : irr.x / albedo.x, albedo.y < 0.01f ? 0.0f : irr.y / albedo.y,
                       albedo.z < 0.01f ? 0.0f : irr.z / albedo.z);
         float sum_variance = 0.0f;
@@ -2370,17 +2384,14 @@ __global__ __launch_bounds__(256) void k_denoise3(FrameArgs A, DenoiseArgs D)
 }
 
 // ------------------------------------------------------------------ tone mapping (tone_mapping.wgsl:21-32)
-__global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
+// one pixel's output texel from its direct, emissive and (has_i) indirect texels
+HKD uint2 tone_texel(const Frame& F, uint2 dv, uint2 ev, uint2 iv, bool has_i)
 {
-    const Frame& F = A.F;
-    int32_t x, y;
-    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
-    const int32_t idx = s_index(F, x, y);
-    f4 c = load_rgba16f(T.direct, idx);
-    f4 e = load_rgba16f(T.emissive, idx);
+    f4 c = mk4(unpack_lo16float(dv.x), unpack_hi16float(dv.x), unpack_lo16float(dv.y), unpack_hi16float(dv.y));
+    const f4 e = mk4(unpack_lo16float(ev.x), unpack_hi16float(ev.x), unpack_lo16float(ev.y), unpack_hi16float(ev.y));
     c = mk4(c.x + e.x, c.y + e.y, c.z + e.z, c.w + e.w);
-    if (T.indirect) {
-        f4 i = load_rgba16f(T.indirect, idx);
+    if (has_i) {
+        const f4 i = mk4(unpack_lo16float(iv.x), unpack_hi16float(iv.x), unpack_lo16float(iv.y), unpack_hi16float(iv.y));
         c = mk4(c.x + i.x, c.y + i.y, c.z + i.z, c.w + i.w);
     }
     f3 cc = vmax(xyz(c), mk3(0.0039f, 0.0039f, 0.0039f));
@@ -2388,7 +2399,45 @@ __global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
     float l_new = l_old / (1.0f + l_old);
     cc = cc * (l_new / l_old);
     f4 o = c.w > 0.0f ? mk4(cc.x, cc.y, cc.z, c.w) : mk4(F.clear_color[0], F.clear_color[1], F.clear_color[2], F.clear_color[3]);
-    store_rgba16f(T.output, idx, o);
+    return make_uint2(pack2x16float(o.x, o.y), pack2x16float(o.z, o.w));
+}
+__global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
+{
+    const Frame& F = A.F;
+    int32_t x, y;
+    if (!tile_pixel<XCD_RASTER>(F, F.s[0], F.s_row0, F.s_rows, x, y)) return;
+    const int32_t idx = s_index(F, x, y);
+    T.output[idx] = tone_texel(F, T.direct[idx], T.emissive[idx], T.indirect ? T.indirect[idx] : make_uint2(0u, 0u),
+                               T.indirect != nullptr);
+}
+// The same over the launch window as runs of 4 pixels of a row (launch_tone, when the plane width and the window's
+// columns are multiples of 4): a texel depends on its own pixel only, so a thread takes 4 consecutive texels of each
+// plane (two 16-byte loads) and a wave 2 KiB of contiguous plane, instead of an 8x8 tile whose rows are 64-byte half
+// lines.  Quad q of the window: local row ly0 + q / quads, columns x0 + 4 (q % quads) ...
+__global__ __launch_bounds__(256) void k_tone4(FrameArgs A, ToneArgs T, int32_t ly0, int32_t x0, uint32_t quads, uint32_t n)
+{
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= n) return;
+    const uint32_t r = q / quads;
+    const int32_t idx = x0 + 4 * (int32_t)(q - r * quads) + (int32_t)A.F.s[0] * (ly0 + (int32_t)r);
+    const uint4* d = reinterpret_cast<const uint4*>(T.direct + idx);
+    const uint4* e = reinterpret_cast<const uint4*>(T.emissive + idx);
+    const uint4 d0 = d[0], d1 = d[1], e0 = e[0], e1 = e[1];
+    uint4 i0 = make_uint4(0u, 0u, 0u, 0u), i1 = i0;
+    const bool has_i = T.indirect != nullptr;
+    if (has_i) {
+        const uint4* i = reinterpret_cast<const uint4*>(T.indirect + idx);
+        i0 = i[0];
+        i1 = i[1];
+    }
+    const Frame& F = A.F;
+    const uint2 o0 = tone_texel(F, make_uint2(d0.x, d0.y), make_uint2(e0.x, e0.y), make_uint2(i0.x, i0.y), has_i);
+    const uint2 o1 = tone_texel(F, make_uint2(d0.z, d0.w), make_uint2(e0.z, e0.w), make_uint2(i0.z, i0.w), has_i);
+    const uint2 o2 = tone_texel(F, make_uint2(d1.x, d1.y), make_uint2(e1.x, e1.y), make_uint2(i1.x, i1.y), has_i);
+    const uint2 o3 = tone_texel(F, make_uint2(d1.z, d1.w), make_uint2(e1.z, e1.w), make_uint2(i1.z, i1.w), has_i);
+    uint4* o = reinterpret_cast<uint4*>(T.output + idx);
+    o[0] = make_uint4(o0.x, o0.y, o1.x, o1.y);
+    o[1] = make_uint4(o2.x, o2.y, o3.x, o3.y);
 }
 
 // ------------------------------------------------------------------ stand-alone ray query
@@ -2691,7 +2740,15 @@ void launch_denoise(const FrameArgs& A, const DenoiseArgs& D, int level, hipStre
 }
 void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_tone, tiles(A.F, A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
+    const Frame& F = A.F;
+    const int32_t ly0 = F.win_rows > 0 ? F.win_row0 : 0, rows = F.win_rows > 0 ? F.win_rows : F.s_rows;
+    const int32_t x0 = F.win_cols > 0 ? F.win_col0 : 0, cols = F.win_cols > 0 ? F.win_cols : (int32_t)F.s[0];
+    if (F.s[0] % 4u == 0u && x0 % 4 == 0 && cols % 4 == 0 && rows > 0 && cols > 0) {
+        const uint32_t quads = (uint32_t)cols / 4u, n = quads * (uint32_t)rows;
+        hipLaunchKernelGGL(k_tone4, dim3((n + 255u) / 256u), dim3(256), 0, st, A, T, ly0, x0, quads, n);
+    } else {
+        hipLaunchKernelGGL(k_tone, tiles(A.F, A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
+    }
 }
 // ------------------------------------------------------------------ sub-frame accumulation
 __global__ __launch_bounds__(256) void k_accumulate(const uint2* tone, float4* acc, uint32_t n, int reset)
