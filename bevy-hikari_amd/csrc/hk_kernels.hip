@@ -2410,34 +2410,38 @@ __global__ __launch_bounds__(256) void k_tone(FrameArgs A, ToneArgs T)
     T.output[idx] = tone_texel(F, T.direct[idx], T.emissive[idx], T.indirect ? T.indirect[idx] : make_uint2(0u, 0u),
                                T.indirect != nullptr);
 }
-// The same over the launch window as runs of 4 pixels of a row (launch_tone, when the plane width and the window's
-// columns are multiples of 4): a texel depends on its own pixel only, so a thread takes 4 consecutive texels of each
-// plane (two 16-byte loads) and a wave 2 KiB of contiguous plane, instead of an 8x8 tile whose rows are 64-byte half
-// lines.  Quad q of the window: local row ly0 + q / quads, columns x0 + 4 (q % quads) ...
-__global__ __launch_bounds__(256) void k_tone4(FrameArgs A, ToneArgs T, int32_t ly0, int32_t x0, uint32_t quads, uint32_t n)
+// The same over the launch window as runs of TONE_RUN pixels of a row (launch_tone, when the plane width and the
+// window's columns are multiples of TONE_RUN): a texel depends on its own pixel only, so a thread takes TONE_RUN
+// consecutive texels of each plane (16-byte loads) and a wave 64 x 8 x TONE_RUN bytes of contiguous plane, instead of
+// an 8x8 tile whose rows are 64-byte half lines.  Run q of the window: local row ly0 + q / runs, columns
+// x0 + TONE_RUN (q % runs) ...
+constexpr int TONE_RUN = 2;  // 2: 0.0143 ms on cornell, 4: 0.0156, 8: 0.0204 (profiles/r06/c19)
+__global__ __launch_bounds__(256) void k_tone_run(FrameArgs A, ToneArgs T, int32_t ly0, int32_t x0, uint32_t runs, uint32_t n)
 {
+    constexpr int V = TONE_RUN / 2;  // 16-byte vectors per plane
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= n) return;
-    const uint32_t r = q / quads;
-    const int32_t idx = x0 + 4 * (int32_t)(q - r * quads) + (int32_t)A.F.s[0] * (ly0 + (int32_t)r);
+    const uint32_t r = q / runs;
+    const int32_t idx = x0 + TONE_RUN * (int32_t)(q - r * runs) + (int32_t)A.F.s[0] * (ly0 + (int32_t)r);
     const uint4* d = reinterpret_cast<const uint4*>(T.direct + idx);
     const uint4* e = reinterpret_cast<const uint4*>(T.emissive + idx);
-    const uint4 d0 = d[0], d1 = d[1], e0 = e[0], e1 = e[1];
-    uint4 i0 = make_uint4(0u, 0u, 0u, 0u), i1 = i0;
+    const uint4* ip = reinterpret_cast<const uint4*>(T.indirect + idx);
     const bool has_i = T.indirect != nullptr;
-    if (has_i) {
-        const uint4* i = reinterpret_cast<const uint4*>(T.indirect + idx);
-        i0 = i[0];
-        i1 = i[1];
+    uint4 dv[V], ev[V], iv[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        dv[k] = d[k];
+        ev[k] = e[k];
+        iv[k] = has_i ? ip[k] : make_uint4(0u, 0u, 0u, 0u);
     }
     const Frame& F = A.F;
-    const uint2 o0 = tone_texel(F, make_uint2(d0.x, d0.y), make_uint2(e0.x, e0.y), make_uint2(i0.x, i0.y), has_i);
-    const uint2 o1 = tone_texel(F, make_uint2(d0.z, d0.w), make_uint2(e0.z, e0.w), make_uint2(i0.z, i0.w), has_i);
-    const uint2 o2 = tone_texel(F, make_uint2(d1.x, d1.y), make_uint2(e1.x, e1.y), make_uint2(i1.x, i1.y), has_i);
-    const uint2 o3 = tone_texel(F, make_uint2(d1.z, d1.w), make_uint2(e1.z, e1.w), make_uint2(i1.z, i1.w), has_i);
     uint4* o = reinterpret_cast<uint4*>(T.output + idx);
-    o[0] = make_uint4(o0.x, o0.y, o1.x, o1.y);
-    o[1] = make_uint4(o2.x, o2.y, o3.x, o3.y);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const uint2 a = tone_texel(F, make_uint2(dv[k].x, dv[k].y), make_uint2(ev[k].x, ev[k].y), make_uint2(iv[k].x, iv[k].y), has_i);
+        const uint2 b = tone_texel(F, make_uint2(dv[k].z, dv[k].w), make_uint2(ev[k].z, ev[k].w), make_uint2(iv[k].z, iv[k].w), has_i);
+        o[k] = make_uint4(a.x, a.y, b.x, b.y);
+    }
 }
 
 // ------------------------------------------------------------------ stand-alone ray query
@@ -2743,9 +2747,9 @@ void launch_tone(const FrameArgs& A, const ToneArgs& T, hipStream_t st)
     const Frame& F = A.F;
     const int32_t ly0 = F.win_rows > 0 ? F.win_row0 : 0, rows = F.win_rows > 0 ? F.win_rows : F.s_rows;
     const int32_t x0 = F.win_cols > 0 ? F.win_col0 : 0, cols = F.win_cols > 0 ? F.win_cols : (int32_t)F.s[0];
-    if (F.s[0] % 4u == 0u && x0 % 4 == 0 && cols % 4 == 0 && rows > 0 && cols > 0) {
-        const uint32_t quads = (uint32_t)cols / 4u, n = quads * (uint32_t)rows;
-        hipLaunchKernelGGL(k_tone4, dim3((n + 255u) / 256u), dim3(256), 0, st, A, T, ly0, x0, quads, n);
+    if (F.s[0] % (uint32_t)TONE_RUN == 0u && x0 % TONE_RUN == 0 && cols % TONE_RUN == 0 && rows > 0 && cols > 0) {
+        const uint32_t runs = (uint32_t)cols / (uint32_t)TONE_RUN, n = runs * (uint32_t)rows;
+        hipLaunchKernelGGL(k_tone_run, dim3((n + 255u) / 256u), dim3(256), 0, st, A, T, ly0, x0, runs, n);
     } else {
         hipLaunchKernelGGL(k_tone, tiles(A.F, A.F.s[0], A.F.s_rows), dim3(256), 0, st, A, T);
     }
