@@ -1643,14 +1643,19 @@ __global__ __launch_bounds__(256) void k_wf_trace(FrameArgs A, ChannelArgs C, Wf
     uint32_t seg, i;
     const bool valid = wf_entry(W, seg, i);
     if ((blockIdx.x / WF_SEGS) * 256u >= W.ctl[seg]) return;  // the whole workgroup is past the count
+    // the queued pixel's texels first (every queued pixel is covered: one round trip, before any staging)
+    int32_t x = 0, y = 0;
+    PixelTexels tex;
+    if (valid) {
+        wf_unpack(A.F, W.queue1[seg * W.seg_cap + i], x, y);
+        tex = load_pixel_texels(A, x, y);
+    }
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
     uint32_t n_top = 0, n_emitter = 0, key = 0;
     if (valid) {
-        int32_t x, y;
-        wf_unpack(A.F, W.queue1[seg * W.seg_cap + i], x, y);
-        indirect_body<false, IND_TRACE>(A, sc, C, x, y, n_top, n_emitter, &W, &key);
+        indirect_body<false, IND_TRACE>(A, sc, C, x, y, n_top, n_emitter, &W, &key, nullptr, &tex);
         if (!counted(A.F, x, y)) n_top = 0;
         W.keys[seg * W.seg_cap + i] = key;
     }
@@ -1703,15 +1708,20 @@ __global__ __launch_bounds__(256) void k_wf_shade(FrameArgs A, ChannelArgs C, Wf
 {
     const uint32_t n = W.ctl[WF_SEGS];
     if (blockIdx.x * 256u >= n) return;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    // the queued pixel's texels first (as k_wf_trace)
+    int32_t x = 0, y = 0;
+    PixelTexels tex;
+    if (i < n) {
+        wf_unpack(A.F, W.queue2[i], x, y);
+        tex = load_pixel_texels(A, x, y);
+    }
     Scene sc;
     if constexpr (LDS) sc = stage_scene<PLAN_LIGHT>(A.sc, hk_lds_scene);
     else sc = A.sc;
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     uint32_t n_top = 0, n_emitter = 0;
     if (i < n) {
-        int32_t x, y;
-        wf_unpack(A.F, W.queue2[i], x, y);
-        indirect_body<false, IND_SHADE>(A, sc, C, x, y, n_top, n_emitter, &W);
+        indirect_body<false, IND_SHADE>(A, sc, C, x, y, n_top, n_emitter, &W, nullptr, nullptr, &tex);
         if (!counted(A.F, x, y)) n_top = n_emitter = 0;
     }
     wave_count(A.cnt.top, n_top);
