@@ -51,10 +51,11 @@ def lds_mode(request, hk_options):
     return request.param
 
 
-@pytest.mark.parametrize("size", [(64, 64), (96, 72), (256, 256)])
+@pytest.mark.parametrize("size", [(64, 64), (96, 72), (63, 47), (256, 256)])
 def test_cornell_frames_bit_exact(size, lds_mode):
     """(256, 256): BASELINE configs[0] (examples/cornell.rs 256x256, all passes incl. spatial reuse
-    and the denoiser)."""
+    and the denoiser).  (63, 47): odd sizes — partial 16x16 tiles on both edges, and the tone pass's
+    tile kernel (k_tone; even widths take the 2-pixel-run kernel)."""
     from hikari_amd import HikariSettings, Upscale, frame_inputs
     w, h = size
     st = HikariSettings(upscale=Upscale.SMAA_TU_1_0)
